@@ -1,0 +1,116 @@
+"""ctypes binding of libdcamd.so (the C ABI in include/dcamd.h).
+
+The library is loaded from the package directory only (in-tree build); there is no fallback:
+if it is missing or was built for another ABI, every hot-path entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent / "libdcamd.so"
+ABI_VERSION = 1
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_longlong
+f32 = C.c_float
+fp = C.POINTER(C.c_float)
+
+
+class ConvDesc(C.Structure):
+    """Mirror of ``dc_conv_desc`` (include/dcamd.h)."""
+
+    _fields_ = [
+        ("x", vp), ("x2", vp), ("ldx", i32), ("ldx2", i32), ("c1", i32),
+        ("nb", i32), ("hin", i32), ("win", i32), ("cin", i32),
+        ("hout", i32), ("wout", i32),
+        ("kh", i32), ("kw", i32), ("stride", i32), ("pad", i32), ("mode", i32),
+        ("w", vp), ("ktot", i32), ("cout", i32),
+        ("bias", vp), ("rowbias", vp), ("rowbias_idx", vp), ("rowbias_ld", i32),
+        ("resid", vp), ("ldr", i32), ("mask", vp), ("ldmask", i32), ("act", i32),
+        ("y", vp), ("ldy", i32),
+        ("ws", vp), ("ws_bytes", i64),
+    ]
+
+
+# name -> argtypes (all return int status unless listed in _RESTYPE)
+_SIGS = {
+    "dc_abi_version": [],
+    "dc_conv_gemm": [C.POINTER(ConvDesc), vp],
+    "dc_groupnorm_ws_bytes": [i32, i32, i32, i32],
+    "dc_groupnorm_fwd": [vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, i32, vp, vp, vp],
+    "dc_groupnorm_bwd": [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp, i32,
+                         vp, i32, vp, vp],
+    "dc_layernorm_fwd": [vp, i32, i64, i32, f32, vp, vp, vp, i32, vp, vp],
+    "dc_layernorm_bwd": [vp, i32, i64, i32, vp, vp, vp, i32, vp, i32, vp, i32, vp],
+    "dc_attn_fwd": [vp, i32, i32, i32, i32, vp, i32, vp, vp],
+    "dc_attn_bwd": [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, i32, vp],
+    "dc_crossattn_fwd": [vp, i32, i64, i32, i32, f32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
+    "dc_crossattn_bwd": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, i32, vp],
+    "dc_geglu_fwd": [vp, i32, i64, i32, vp, i32, vp],
+    "dc_geglu_bwd": [vp, i32, i64, i32, vp, i32, vp, i32, vp],
+    "dc_upsample_adjoint": [vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp],
+    "dc_taesd_clamp_fwd": [vp, i32, i64, vp, vp],
+    "dc_taesd_clamp_bwd": [vp, i32, vp, i32, i64, vp, vp, vp, vp, vp],
+    "dc_silu": [vp, i64, vp, vp],
+    "dc_preprocess_image": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp],
+    "dc_nhwc_to_nchw": [vp, i32, i32, i64, i32, vp, vp],
+    "dc_nchw_to_nhwc": [vp, i32, i64, i32, vp, i32, vp],
+    "dc_sparse_setup": [vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp, vp, vp, vp, vp],
+    "dc_preview": [vp, vp, i32, i32, vp, vp, vp, vp, vp, vp],
+    "dc_sparse_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "dc_decode_tail_bwd": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp],
+    "dc_latent_update": [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "dc_step_advance": [vp, vp],
+    "dc_latent_init": [vp, vp, f32, i32, i32, vp, vp],
+    "dc_final_dense": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
+    "dc_memset_async": [vp, i32, i64, vp],
+}
+_RESTYPE = {"dc_groupnorm_ws_bytes": i64}
+
+STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}
+
+
+class DCError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib_path() -> Path:
+    return _LIB_PATH
+
+
+def load():
+    """Load libdcamd.so once; raises if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not _LIB_PATH.exists():
+        raise DCError(f"{_LIB_PATH} not found: build it with `python -m depth_completion_amd.build` "
+                      "(the HIP extension is required; there is no fallback path)")
+    lib = C.CDLL(str(_LIB_PATH))
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, i32)
+    if lib.dc_abi_version() != ABI_VERSION:
+        raise DCError(f"libdcamd ABI {lib.dc_abi_version()} != expected {ABI_VERSION}; rebuild")
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGS)
+
+
+def check(status: int, name: str):
+    if status != 0:
+        raise DCError(f"{name} failed: {STATUS.get(status, status)}")
+
+
+def call(name: str, *args):
+    st = getattr(load(), name)(*args)
+    check(st, name)

@@ -1,0 +1,59 @@
+"""Build libdcamd.so (all HIP kernels + the C ABI of include/dcamd.h) for gfx950, in-tree.
+
+``python -m depth_completion_amd.build`` or ``__graft_entry__.build()``.  hipcc cross-compiles
+without a GPU, so this runs in the CPU container too.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libdcamd.so"
+OBJ_DIR = PKG / "build_obj"
+SOURCES = ["conv_gemm.hip", "norms.hip", "attention.hip", "elementwise.hip", "guidance.hip", "version.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("DC_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def _needs(obj: Path, deps: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> Path:
+    OBJ_DIR.mkdir(exist_ok=True)
+    headers = [CSRC / "common.h", PKG.parent / "include" / "dcamd.h"]
+    jobs = []
+    for src in SOURCES:
+        s = CSRC / src
+        o = OBJ_DIR / (src + ".o")
+        if force or _needs(o, [s, *headers]):
+            jobs.append([HIPCC, *FLAGS, "-c", str(s), "-o", str(o)])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r
+
+    with ThreadPoolExecutor(max_workers=min(len(jobs), 6) or 1) as ex:
+        list(ex.map(run, jobs))
+    objs = [str(OBJ_DIR / (s + ".o")) for s in SOURCES]
+    if force or jobs or not LIB.exists():
+        run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", str(LIB), *objs])
+    return LIB
+
+
+if __name__ == "__main__":
+    p = build(verbose=True, force="--force" in sys.argv)
+    print("built", p)

@@ -1,0 +1,492 @@
+// The sparse-depth guidance of one guided DDIM step (marigold_dc.py:806-904) as fused gfx950 kernels.
+//
+//   dc_sparse_setup     once per call: compact LiDAR pixels (sparses > 0) per frame, sparse
+//                       normalisation (marigold_dc.py:706-756), masked min/max of the guides
+//                       (utils.py:89-138 as used by _affine_to_metric, marigold_dc.py:326)
+//   dc_preview          Tweedie preview x0 = sqrt(a)x - sqrt(1-a)v, TAESD clamp input tanh(x0/3)*3,
+//                       ||eps||, eps = sqrt(a)v + sqrt(1-a)x      (marigold_dc.py:813-826)
+//   dc_sparse_loss      decode tail (x*2-1, channel mean, clip, (x+1)/2), bilinear resize at the
+//                       sparse pixels only, learned affine + clamp, l1+l2 loss, its gradient
+//                       scattered into the decoded-depth image, d(scale), d(shift)  (:829-877)
+//   dc_decode_tail_bwd  gradient of the decode tail back to the TAESD decoder output
+//   dc_latent_update    grad accumulation, ||eps||/||g|| rescale, Adam (bf16 state for the latent,
+//                       fp32 for scale/shift), DDIM prev-sample on the post-Adam latent (:879-904)
+//   dc_final_dense      final decode -> affine -> clamp -> metres (:969-985)
+// Elementwise arithmetic mirrors PyTorch's op-by-op rounding (bf16 results of bf16 ops, fp32 for
+// the affine/loss), so the only deviation from the reference is reduction order.
+#include "common.h"
+#include "../../include/dcamd.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int SETUP_THREADS = 1024;
+
+__device__ __forceinline__ float proj_f(float v, int projection) {
+  if (projection == 1) return logf(v);
+  if (projection == 2) return log10f(v);
+  return v;
+}
+
+__device__ float block_min(float v, float* scratch) {
+  for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float t = l < nw ? scratch[l] : INFINITY;
+  for (int o = 32; o >= 1; o >>= 1) t = fminf(t, __shfl_xor(t, o, 64));
+  return t;
+}
+__device__ float block_max(float v, float* scratch) { return -block_min(-v, scratch); }
+
+// params per frame: [0]=lo [1]=hi (metres) [2]=lo_p [3]=hi_p [4]=min_g [5]=max_g
+__global__ void sparse_setup_kernel(const float* sparse, int H, int W, int norm, float min_depth, float max_depth,
+                                    const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt,
+                                    float* params) {
+  __shared__ int wave_counts[SETUP_THREADS / 64];
+  __shared__ float scratch[SETUP_THREADS / 64];
+  __shared__ int base_sh;
+  const int n = blockIdx.x;
+  const long HW = (long)H * W;
+  const float* sp = sparse + n * HW;
+  int* ix = idx + n * HW;
+  float* gv = gval + n * HW;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (threadIdx.x == 0) base_sh = 0;
+  float rmin = INFINITY, rmax = -INFINITY;
+  __syncthreads();
+  for (long p0 = 0; p0 < HW; p0 += blockDim.x) {
+    const long p = p0 + threadIdx.x;
+    const float v = p < HW ? sp[p] : 0.0f;
+    const bool f = v > 0.0f;
+    if (f) { rmin = fminf(rmin, v); rmax = fmaxf(rmax, v); }
+    const unsigned long long bal = __ballot(f);
+    const int before = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_counts[w] = __popcll(bal);
+    __syncthreads();
+    int off = base_sh;
+    for (int k = 0; k < w; ++k) off += wave_counts[k];
+    if (f) {
+      ix[off + before] = (int)p;
+      gv[off + before] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int k = 0; k < nw; ++k) tot += wave_counts[k];
+      base_sh += tot;
+    }
+    __syncthreads();
+  }
+  const int count = base_sh;
+  rmin = block_min(rmin, scratch);
+  rmax = block_max(rmax, scratch);
+  float lo, hi;
+  if (norm == 0) {           // const
+    lo = min_depth;
+    hi = max_depth;
+  } else if (norm == 1) {    // minmax
+    lo = rmin;
+    hi = rmax;
+  } else {                   // percentile: provided by the host (quantiles of the masked values)
+    lo = host_lohi[2 * n];
+    hi = host_lohi[2 * n + 1];
+  }
+  const float lo_c = lo, hi_c = hi;  // sparses.clamp(min=lo, max=hi) uses the un-clamped range
+  if (norm != 0) {
+    lo = fmaxf(lo, min_depth);
+    hi = fminf(hi, max_depth);
+  }
+  float lo_p = proj_f(lo, projection), hi_p = proj_f(hi, projection);
+  if (inv) {
+    const float a = 1.0f / hi_p, b = 1.0f / lo_p;
+    lo_p = a;
+    hi_p = b;
+  }
+  float gmin = INFINITY, gmax = -INFINITY;
+  __syncthreads();
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    float v = fminf(fmaxf(gv[k], lo_c), hi_c);
+    v = proj_f(v, projection);
+    if (inv) v = 1.0f / v;
+    const float g = (v - lo_p) / (hi_p - lo_p);
+    gv[k] = g;
+    gmin = fminf(gmin, g);
+    gmax = fmaxf(gmax, g);
+  }
+  gmin = block_min(gmin, scratch);
+  gmax = block_max(gmax, scratch);
+  if (threadIdx.x == 0) {
+    cnt[n] = count;
+    float* pr = params + n * 8;
+    pr[0] = lo; pr[1] = hi; pr[2] = lo_p; pr[3] = hi_p; pr[4] = gmin; pr[5] = gmax;
+    pr[6] = (float)count; pr[7] = 0.0f;
+  }
+}
+
+// coef table per step: [sqrt(a_t), sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev)]
+__global__ void preview_kernel(const bf16* x8, const bf16* v, int hw, const float* coef, const int* step, bf16* x0,
+                               bf16* tin, float* eps_norm) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.x;
+  const float sa = coef[*step * 4 + 0], sb = coef[*step * 4 + 1];
+  float ss = 0.0f;
+  for (int p = threadIdx.x; p < hw; p += blockDim.x) {
+    const long pix = (long)n * hw + p;
+    float xo[8], to[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x = (float)x8[pix * 8 + 4 + k];
+      const float vv = (float)v[pix * 8 + k];
+      const float t1 = (float)(bf16)(sa * x), t2 = (float)(bf16)(sb * vv);
+      const float xz = (float)(bf16)(t1 - t2);
+      const float e = (float)(bf16)((float)(bf16)(sa * vv) + (float)(bf16)(sb * x));
+      ss += e * e;
+      xo[k] = xz;
+      xo[k + 4] = 0.0f;
+      const float a = (float)(bf16)(xz / 3.0f);
+      to[k] = (float)(bf16)((float)(bf16)tanhf(a) * 3.0f);
+      to[k + 4] = 0.0f;
+    }
+    store8(x0 + pix * 8, xo);
+    store8(tin + pix * 8, to);
+  }
+  const float tot = block_sum(ss, scratch);
+  if (threadIdx.x == 0) eps_norm[n] = (float)(bf16)sqrtf(tot);
+}
+
+// decoded-affine value A at processing-res pixel (y, x): decode tail of TAESD output `out` [PH*PW][ldo]
+__device__ __forceinline__ float decode_tail(const bf16* out, int ldo, long pix) {
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) s += (float)(bf16)((float)(bf16)((float)out[pix * ldo + c] * 2.0f) - 1.0f);
+  const float mean = (float)(bf16)(s * (1.0f / 3.0f));
+  const float cl = fminf(fmaxf(mean, -1.0f), 1.0f);
+  return (float)(bf16)((float)(bf16)(cl + 1.0f) / 2.0f);
+}
+
+struct Taps {
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+};
+// upsample_bilinear2d (align_corners=False, no antialias) source taps for output (y,x): in (RH,RW) -> out (H,W)
+__device__ __forceinline__ Taps bilinear_taps(int y, int x, int RH, int RW, int H, int W) {
+  Taps t;
+  const float rh = (float)RH / H, rw = (float)RW / W;
+  float sy = rh * (y + 0.5f) - 0.5f;
+  sy = sy < 0.0f ? 0.0f : sy;
+  float sx = rw * (x + 0.5f) - 0.5f;
+  sx = sx < 0.0f ? 0.0f : sx;
+  t.y0 = (int)sy;
+  t.x0 = (int)sx;
+  t.y1 = t.y0 + ((t.y0 < RH - 1) ? 1 : 0);
+  t.x1 = t.x0 + ((t.x0 < RW - 1) ? 1 : 0);
+  t.ly1 = sy - t.y0;
+  t.ly0 = 1.0f - t.ly1;
+  t.lx1 = sx - t.x0;
+  t.lx0 = 1.0f - t.lx1;
+  return t;
+}
+
+__device__ __forceinline__ float sample_affine(const bf16* out, int ldo, int n, int PH, int PW, int RH, int RW, int H,
+                                               int W, int y, int x, Taps& t) {
+  const long base = (long)n * PH * PW;
+  if (RH == H && RW == W) {
+    t.y0 = t.y1 = y;
+    t.x0 = t.x1 = x;
+    t.ly0 = t.lx0 = 1.0f;
+    t.ly1 = t.lx1 = 0.0f;
+    return decode_tail(out, ldo, base + (long)y * PW + x);
+  }
+  t = bilinear_taps(y, x, RH, RW, H, W);
+  const float a00 = decode_tail(out, ldo, base + (long)t.y0 * PW + t.x0);
+  const float a01 = decode_tail(out, ldo, base + (long)t.y0 * PW + t.x1);
+  const float a10 = decode_tail(out, ldo, base + (long)t.y1 * PW + t.x0);
+  const float a11 = decode_tail(out, ldo, base + (long)t.y1 * PW + t.x1);
+  const float v = t.ly0 * (t.lx0 * a00 + t.lx1 * a01) + t.ly1 * (t.lx0 * a10 + t.lx1 * a11);
+  return (float)(bf16)v;
+}
+
+// one block per frame.  affine[n*2] = scale, affine[n*2+1] = shift (fp32 trainables)
+__global__ void sparse_loss_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
+                                   const int* idx, const float* gval, const int* cnt, const float* params,
+                                   const float* affine, float* dA, float* daff_grad, float* loss) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.x;
+  const long HW = (long)H * W;
+  const int count = cnt[n];
+  const float* pr = params + n * 8;
+  const float gmin = pr[4], gmax = pr[5];
+  const float s = affine[n * 2], sh = affine[n * 2 + 1];
+  const float A1 = s * s;
+  const float B = A1 * (gmax - gmin);
+  const float E = (sh * sh) * gmin;
+  const float inv_cnt = 1.0f / (float)count;
+  float sum_db = 0.0f, sum_de = 0.0f, lsum = 0.0f;
+  float* dAn = dA + (long)n * PH * PW;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    const int p = idx[n * HW + k];
+    const int y = p / W, x = p - (p / W) * W;
+    Taps t;
+    const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t);
+    const float F = B * aff + E;
+    const float G = fminf(fmaxf(F, 0.0f), 1.0f);
+    const float r = G - gval[n * HW + k];
+    lsum += fabsf(r) * inv_cnt + (r * r) * inv_cnt;
+    const float sg = (r > 0.0f) ? 1.0f : ((r < 0.0f) ? -1.0f : 0.0f);
+    const float dG = sg * inv_cnt + 2.0f * r * inv_cnt;
+    const float dF = (F >= 0.0f && F <= 1.0f) ? dG : 0.0f;
+    sum_db += dF * aff;
+    sum_de += dF;
+    const float dff = (float)(bf16)(dF * B);
+    if (t.ly1 == 0.0f && t.lx1 == 0.0f && t.y0 == t.y1 && t.x0 == t.x1) {
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x0], dff);
+    } else {
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x0], t.ly0 * t.lx0 * dff);
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x1], t.ly0 * t.lx1 * dff);
+      atomicAdd(&dAn[(long)t.y1 * PW + t.x0], t.ly1 * t.lx0 * dff);
+      atomicAdd(&dAn[(long)t.y1 * PW + t.x1], t.ly1 * t.lx1 * dff);
+    }
+  }
+  const float db = block_sum(sum_db, scratch);
+  __syncthreads();
+  const float de = block_sum(sum_de, scratch);
+  __syncthreads();
+  const float ls = block_sum(lsum, scratch);
+  if (threadIdx.x == 0) {
+    const float dA1 = db * (gmax - gmin);
+    daff_grad[n * 2] = dA1 * (2.0f * s);
+    daff_grad[n * 2 + 1] = (de * gmin) * (2.0f * sh);
+    loss[n] = ls;
+  }
+}
+
+// dA (fp32, [nb][PH][PW]) -> gradient of the TAESD decoder output (bf16 [P][8], channels 0..2)
+__global__ void decode_tail_bwd_kernel(const bf16* out, int ldo, const float* dA, int nb, int PH, int PW, int RH,
+                                       int RW, bf16* dout) {
+  const long total = (long)nb * PH * PW;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % PW);
+    const int y = (int)((i / PW) % PH);
+    float g = 0.0f;
+    if (y < RH && x < RW) {
+      g = (float)(bf16)dA[i];
+      if (g != 0.0f) {
+        g = (float)(bf16)(g / 2.0f);
+        float s = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) s += (float)(bf16)((float)(bf16)((float)out[i * ldo + c] * 2.0f) - 1.0f);
+        const float mean = (float)(bf16)(s * (1.0f / 3.0f));
+        g = (mean >= -1.0f && mean <= 1.0f) ? g : 0.0f;
+        g = (float)(bf16)(g / 3.0f);
+        g = (float)(bf16)(g * 2.0f);
+      }
+    }
+    float o[8] = {g, g, g, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    store8(dout + i * 8, o);
+  }
+}
+
+// adam_tab per step: [step_size = lr_lat/bc1, bc2_sqrt, step_size_aff = lr_aff/bc1, unused]
+__global__ void latent_update_kernel(bf16* x8, const bf16* v, const bf16* gdir, const bf16* gunet, int hw,
+                                     const float* coef, const float* adam_tab, const int* step,
+                                     const float* eps_norm, bf16* m_lat, bf16* v_lat, float* affine,
+                                     float* m_aff, float* v_aff, const float* daff_grad, float* dbg) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.x;
+  const int st = *step;
+  const float sa = coef[st * 4 + 0], sb = coef[st * 4 + 1], sap = coef[st * 4 + 2], sbp = coef[st * 4 + 3];
+  const float step_size = adam_tab[st * 4 + 0], bc2s = adam_tab[st * 4 + 1], step_aff = adam_tab[st * 4 + 2];
+  const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
+  // pass 1: ||g||
+  float ss = 0.0f;
+  for (int i = threadIdx.x; i < hw * 4; i += blockDim.x) {
+    const long pix = (long)n * hw + (i >> 2);
+    const int k = i & 3;
+    const float g = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
+    ss += g * g;
+  }
+  const float gn = (float)(bf16)sqrtf(block_sum(ss, scratch));
+  const float en = eps_norm[n];
+  const float gnc = gn < 1e-7f ? (float)(bf16)1e-7f : gn;
+  const float factor = (float)(bf16)(en / gnc);
+  // pass 2: rescale, Adam (bf16 state), DDIM update with the pre-update v
+  for (int i = threadIdx.x; i < hw * 4; i += blockDim.x) {
+    const long pix = (long)n * hw + (i >> 2);
+    const int k = i & 3;
+    const long e = pix * 4 + k;
+    float g = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
+    g = (float)(bf16)(g * factor);
+    float m = (float)m_lat[e], vv = (float)v_lat[e];
+    m = (float)(bf16)(m + beta1w * (g - m));
+    vv = (float)(bf16)(vv * beta2);
+    vv = (float)(bf16)(vv + one_m_b2 * g * g);
+    m_lat[e] = (bf16)m;
+    v_lat[e] = (bf16)vv;
+    float den = (float)(bf16)sqrtf(vv);
+    den = (float)(bf16)(den / bc2s);
+    den = (float)(bf16)(den + eps);
+    const float x = (float)x8[pix * 8 + 4 + k];
+    const float xp = (float)(bf16)(x + (-step_size) * (m / den));
+    const float vm = (float)v[pix * 8 + k];
+    const float x0 = (float)(bf16)((float)(bf16)(sa * xp) - (float)(bf16)(sb * vm));
+    const float ep = (float)(bf16)((float)(bf16)(sa * vm) + (float)(bf16)(sb * xp));
+    const float dir = (float)(bf16)(sbp * ep);
+    const float prev = (float)(bf16)((float)(bf16)(sap * x0) + dir);
+    x8[pix * 8 + 4 + k] = (bf16)prev;
+  }
+  if (threadIdx.x < 2) {
+    // Adam on scale (0) / shift (1), fp32
+    const int j = threadIdx.x;
+    const float g = daff_grad[n * 2 + j];
+    float m = m_aff[n * 2 + j], vv = v_aff[n * 2 + j];
+    m = m + beta1w * (g - m);
+    vv = vv * beta2;
+    vv = vv + one_m_b2 * g * g;
+    m_aff[n * 2 + j] = m;
+    v_aff[n * 2 + j] = vv;
+    float den = sqrtf(vv);
+    den = den / bc2s;
+    den = den + eps;
+    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (m / den);
+  }
+  if (dbg && threadIdx.x == 0) {
+    dbg[n * 4 + 0] = gn;
+    dbg[n * 4 + 1] = factor;
+  }
+}
+
+__global__ void step_advance_kernel(int* step) { *step += 1; }
+
+// initial depth latents (marigold_dc.py:677-704): noise [1][4][hw] (NCHW, repeated over frames),
+// optional warm start beta*noise + (1-beta)*prev (prev [nb][4][hw]) -> x8[...,4:8]
+__global__ void latent_init_kernel(const bf16* noise, const bf16* prev, float beta, int nb, int hw, bf16* x8) {
+  const long total = (long)nb * hw * 4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int p = (int)(i % hw);
+    const int k = (int)((i / hw) % 4);
+    const long n = i / ((long)hw * 4);
+    float v = (float)noise[(long)k * hw + p];
+    if (prev) {
+      const float a = (float)(bf16)(beta * v);
+      const float b = (float)(bf16)((1.0f - beta) * (float)prev[i]);
+      v = (float)(bf16)(a + b);
+    }
+    x8[(n * hw + p) * 8 + 4 + k] = (bf16)v;
+  }
+}
+
+// final dense depth: [nb][1][H][W] fp32 metres
+__global__ void final_dense_kernel(const bf16* out, int ldo, int nb, int PH, int PW, int RH, int RW, int H, int W,
+                                   const float* params, const float* affine, float* dense) {
+  const long total = (long)nb * H * W;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % W);
+    const int y = (int)((i / W) % H);
+    const int n = (int)(i / ((long)H * W));
+    Taps t;
+    const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t);
+    const float* pr = params + n * 8;
+    const float s = affine[n * 2], sh = affine[n * 2 + 1];
+    const float B = (s * s) * (pr[5] - pr[4]);
+    const float F = B * aff + (sh * sh) * pr[4];
+    const float G = fminf(fmaxf(F, 0.0f), 1.0f);
+    dense[i] = G * (pr[1] - pr[0]) + pr[0];
+  }
+}
+
+inline dim3 grid_for(long n) {
+  long b = (n + 255) / 256;
+  if (b > 65536) b = 65536;
+  return dim3((unsigned)(b < 1 ? 1 : b));
+}
+
+}  // namespace
+
+extern "C" int dc_sparse_setup(const float* sparse, int nb, int h, int w, int norm, float min_depth, float max_depth,
+                               const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt,
+                               float* params, void* stream) {
+  if (!sparse || !idx || !gval || !cnt || !params || nb <= 0 || h <= 0 || w <= 0) return DC_ERR_ARG;
+  if (norm < 0 || norm > 2 || projection < 0 || projection > 2) return DC_ERR_ARG;
+  if (norm == 2 && !host_lohi) return DC_ERR_ARG;
+  hipLaunchKernelGGL(sparse_setup_kernel, dim3(nb), dim3(SETUP_THREADS), 0, (hipStream_t)stream, sparse, h, w, norm,
+                     min_depth, max_depth, host_lohi, projection, inv, idx, gval, cnt, params);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_preview(const void* x8, const void* v, int nb, int hw, const float* coef, const int* step, void* x0,
+                          void* tin, float* eps_norm, void* stream) {
+  if (!x8 || !v || !coef || !step || !x0 || !tin || !eps_norm || nb <= 0 || hw <= 0) return DC_ERR_ARG;
+  hipLaunchKernelGGL(preview_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, (const bf16*)x8, (const bf16*)v, hw,
+                     coef, step, (bf16*)x0, (bf16*)tin, eps_norm);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_sparse_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                              const int* idx, const float* gval, const int* cnt, const float* params,
+                              const float* affine, float* dA, float* daff_grad, float* loss, void* stream) {
+  if (!dec_out || !idx || !gval || !cnt || !params || !affine || !dA || !daff_grad || !loss) return DC_ERR_ARG;
+  if (nb <= 0 || rh > ph || rw > pw || h <= 0 || w <= 0) return DC_ERR_ARG;
+  hipLaunchKernelGGL(sparse_loss_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
+                     pw, rh, rw, h, w, idx, gval, cnt, params, affine, dA, daff_grad, loss);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_decode_tail_bwd(const void* dec_out, int ldo, const float* dA, int nb, int ph, int pw, int rh,
+                                  int rw, void* dout, void* stream) {
+  if (!dec_out || !dA || !dout || nb <= 0) return DC_ERR_ARG;
+  hipLaunchKernelGGL(decode_tail_bwd_kernel, grid_for((long)nb * ph * pw), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)dec_out, ldo, dA, nb, ph, pw, rh, rw, (bf16*)dout);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gunet, int nb, int hw,
+                                const float* coef, const float* adam_tab, const int* step, const float* eps_norm,
+                                void* m_lat, void* v_lat, float* affine, float* m_aff, float* v_aff,
+                                const float* daff_grad, float* dbg, void* stream) {
+  if (!x8 || !v || !gdir || !gunet || !coef || !adam_tab || !step || !eps_norm || !m_lat || !v_lat || !affine ||
+      !m_aff || !v_aff || !daff_grad || nb <= 0 || hw <= 0)
+    return DC_ERR_ARG;
+  hipLaunchKernelGGL(latent_update_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, (bf16*)x8, (const bf16*)v,
+                     (const bf16*)gdir, (const bf16*)gunet, hw, coef, adam_tab, step, eps_norm, (bf16*)m_lat,
+                     (bf16*)v_lat, affine, m_aff, v_aff, daff_grad, dbg);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_step_advance(int* step, void* stream) {
+  if (!step) return DC_ERR_ARG;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8,
+                              void* stream) {
+  if (!noise || !x8 || nb <= 0 || hw <= 0) return DC_ERR_ARG;
+  hipLaunchKernelGGL(latent_init_kernel, grid_for((long)nb * hw * 4), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)noise, (const bf16*)prev, beta, nb, hw, (bf16*)x8);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                              const float* params, const float* affine, float* dense, void* stream) {
+  if (!dec_out || !params || !affine || !dense || nb <= 0) return DC_ERR_ARG;
+  hipLaunchKernelGGL(final_dense_kernel, grid_for((long)nb * h * w), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)dec_out, ldo, nb, ph, pw, rh, rw, h, w, params, affine, dense);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_memset_async(void* ptr, int value, long long bytes, void* stream) {
+  if (!ptr || bytes < 0) return DC_ERR_ARG;
+  if (hipMemsetAsync(ptr, value, (size_t)bytes, (hipStream_t)stream) != hipSuccess) return DC_ERR_LAUNCH;
+  return DC_OK;
+}

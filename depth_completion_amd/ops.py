@@ -1,0 +1,186 @@
+"""Thin host wrappers: torch device tensors -> raw pointers -> libdcamd.so entry points.
+
+Tensors are 2-D "row" views ``[rows, ld]`` (NHWC pixel rows or token rows).  ``Slice`` carries
+a column offset into a row buffer (for concat halves and q/k/v blocks) without copying.
+PyTorch is used only for device memory and the current stream handle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import ConvDesc, call
+
+BF16 = torch.bfloat16
+
+
+@dataclass
+class Slice:
+    t: torch.Tensor
+    col: int = 0
+
+    @property
+    def ld(self) -> int:
+        return self.t.shape[-1]
+
+    @property
+    def ptr(self) -> int:
+        return self.t.data_ptr() + self.col * self.t.element_size()
+
+
+def S(t, col: int = 0) -> Slice:
+    return t if isinstance(t, Slice) else Slice(t, col)
+
+
+def P(t) -> int | None:
+    """Raw device pointer of a tensor / Slice / None."""
+    if t is None:
+        return None
+    if isinstance(t, Slice):
+        return t.ptr
+    return t.data_ptr()
+
+
+def LD(t) -> int:
+    if t is None:
+        return 0
+    return t.ld if isinstance(t, Slice) else t.shape[-1]
+
+
+class Ctx:
+    """Execution context: stream, fp32 scratch workspace and the device step counter."""
+
+    def __init__(self, device, ws_mb: int = 96):
+        self.device = torch.device(device)
+        self.ws = torch.empty(ws_mb * (1 << 20) // 4, dtype=torch.float32, device=self.device)
+        self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    @property
+    def stream(self) -> int:
+        if self.device.type != "cuda":
+            return 0  # host-side dry runs (tests/test_host_plans.py) only
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    @property
+    def ws_bytes(self) -> int:
+        return self.ws.numel() * 4
+
+
+# ------------------------------------------------------------------------- conv / linear
+def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin: int, hout: int, wout: int,
+              cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
+              c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
+              y=None, splitk: bool = True):
+    d = ConvDesc()
+    d.x = P(x)
+    d.ldx = LD(x)
+    d.x2 = P(x2)
+    d.ldx2 = LD(x2)
+    d.c1 = c1
+    d.nb, d.hin, d.win, d.cin, d.hout, d.wout = nb, hin, win, cin, hout, wout
+    d.kh, d.kw, d.stride, d.pad, d.mode = kh, kw, stride, pad, mode
+    d.w = w.data_ptr()
+    d.ktot = w.shape[1]
+    d.cout = cout
+    d.bias = P(bias)
+    d.rowbias = P(rowbias)
+    d.rowbias_idx = ctx.step.data_ptr() if rowbias is not None else None
+    d.rowbias_ld = rowbias_ld
+    d.resid = P(resid)
+    d.ldr = LD(resid)
+    d.mask = P(mask)
+    d.ldmask = LD(mask)
+    d.act = act
+    d.y = P(y)
+    d.ldy = LD(y)
+    d.ws = ctx.ws.data_ptr() if splitk else None
+    d.ws_bytes = ctx.ws_bytes if splitk else 0
+    call("dc_conv_gemm", C.byref(d), ctx.stream)
+    return y
+
+
+def linear(ctx: Ctx, x, w: torch.Tensor, rows: int, cout: int, y, bias=None, resid=None, rowbias=None,
+           rowbias_ld: int = 0, act: int = 0):
+    """y[rows, cout] = x[rows, K] @ w[cout, K]^T (+ bias, + resid)."""
+    return conv_gemm(ctx, x, w, nb=1, hin=1, win=rows, cin=w.shape[1], hout=1, wout=rows, cout=cout, kh=1, kw=1,
+                     stride=1, pad=0, bias=bias, resid=resid, rowbias=rowbias, rowbias_ld=rowbias_ld, act=act, y=y)
+
+
+# ------------------------------------------------------------------------- norms
+def groupnorm(ctx: Ctx, x, nb, hw, c, gamma, beta, eps, silu, y, stats, x2=None, c1=0, groups=32):
+    call("dc_groupnorm_fwd", P(x), LD(x), P(x2), LD(x2), c1, nb, hw, c, groups, eps, gamma.data_ptr(),
+         beta.data_ptr(), int(silu), P(y), LD(y), stats.data_ptr(), ctx.ws.data_ptr(), ctx.stream)
+    return y
+
+
+def groupnorm_bwd(ctx: Ctx, x, nb, hw, c, gamma, beta, silu, stats, dy, dx, x2=None, c1=0, add1=None, add2=None,
+                  groups=32):
+    call("dc_groupnorm_bwd", P(x), LD(x), P(x2), LD(x2), c1, nb, hw, c, groups, gamma.data_ptr(), beta.data_ptr(),
+         int(silu), stats.data_ptr(), P(dy), LD(dy), P(dx), LD(dx), P(add1), LD(add1), P(add2), LD(add2),
+         ctx.ws.data_ptr(), ctx.stream)
+    return dx
+
+
+def layernorm(ctx: Ctx, x, rows, c, gamma, beta, eps, y, stats):
+    call("dc_layernorm_fwd", P(x), LD(x), rows, c, eps, gamma.data_ptr(), beta.data_ptr(), P(y), LD(y),
+         stats.data_ptr(), ctx.stream)
+    return y
+
+
+def layernorm_bwd(ctx: Ctx, x, rows, c, gamma, stats, dy, dx, add=None):
+    call("dc_layernorm_bwd", P(x), LD(x), rows, c, gamma.data_ptr(), stats.data_ptr(), P(dy), LD(dy), P(dx), LD(dx),
+         P(add), LD(add), ctx.stream)
+    return dx
+
+
+# ------------------------------------------------------------------------- attention
+def attn_fwd(ctx: Ctx, qkv, nb, t, heads, o, lse):
+    call("dc_attn_fwd", P(qkv), LD(qkv), nb, t, heads, P(o), LD(o), lse.data_ptr(), ctx.stream)
+    return o
+
+
+def attn_bwd(ctx: Ctx, qkv, o, dout, lse, nb, t, heads, delta, dqkv):
+    call("dc_attn_bwd", P(qkv), LD(qkv), P(o), LD(o), P(dout), LD(dout), lse.data_ptr(), nb, t, heads,
+         delta.data_ptr(), P(dqkv), LD(dqkv), ctx.stream)
+    return dqkv
+
+
+def crossattn_fwd(ctx: Ctx, x, rows, c, heads, eps, gamma, beta, U, D, c0, y, stats, probs):
+    call("dc_crossattn_fwd", P(x), LD(x), rows, c, heads, eps, gamma.data_ptr(), beta.data_ptr(), U.data_ptr(),
+         D.data_ptr(), c0.data_ptr(), P(y), LD(y), stats.data_ptr(), probs.data_ptr(), ctx.stream)
+    return y
+
+
+def crossattn_bwd(ctx: Ctx, x, rows, c, heads, gamma, U, D, stats, probs, dy, dx):
+    call("dc_crossattn_bwd", P(x), LD(x), rows, c, heads, gamma.data_ptr(), U.data_ptr(), D.data_ptr(),
+         stats.data_ptr(), probs.data_ptr(), P(dy), LD(dy), P(dx), LD(dx), ctx.stream)
+    return dx
+
+
+# ------------------------------------------------------------------------- elementwise
+def geglu(ctx: Ctx, f, rows, c, y):
+    call("dc_geglu_fwd", P(f), LD(f), rows, c, P(y), LD(y), ctx.stream)
+    return y
+
+
+def geglu_bwd(ctx: Ctx, f, rows, c, dy, df):
+    call("dc_geglu_bwd", P(f), LD(f), rows, c, P(dy), LD(dy), P(df), LD(df), ctx.stream)
+    return df
+
+
+def upsample_adjoint(ctx: Ctx, dhi, nb, hhi, whi, c, hlo, wlo, dlo, mask=None):
+    call("dc_upsample_adjoint", P(dhi), LD(dhi), nb, hhi, whi, c, hlo, wlo, P(dlo), LD(dlo), P(mask), LD(mask),
+         ctx.stream)
+    return dlo
+
+
+def silu(ctx: Ctx, x, y):
+    call("dc_silu", P(x), x.numel(), P(y), ctx.stream)
+    return y
+
+
+def memset(ctx: Ctx, t: torch.Tensor, value: int = 0):
+    call("dc_memset_async", t.data_ptr(), value, t.numel() * t.element_size(), ctx.stream)

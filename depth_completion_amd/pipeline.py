@@ -1,0 +1,344 @@
+"""MI355X-native ``MarigoldDepthCompletionPipeline`` -- drop-in for marigold_dc.py:248-985.
+
+Same ``__call__`` signature, defaults and ValueError behaviour as the reference (marigold_dc.py:
+467-656); the guided DDIM loop runs entirely in libdcamd.so kernels (UNet fwd + input-gradient,
+TAESD decoder fwd + input-gradient, fused guidance/Adam/DDIM), one step captured in a hipGraph
+and replayed for every timestep.  There is no CPU or PyTorch-op fallback: if the HIP library is
+missing, construction fails.
+
+Deviations (documented in DESIGN.md):
+* the initial noise is drawn from a CPU ``torch.Generator`` seeded with ``seed`` (the reference
+  draws it from a device Philox generator, marigold_dc.py:661, 677-684), so CPU and GPU runs
+  share it; an explicit ``init_noise`` may be passed;
+* latent dims follow the padded preprocessing size (the reference crashes when the resized short
+  side is not a multiple of 8);
+* the empty-prompt text embedding is a constant supplied at construction.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from .config import MARIGOLD_V1, UNetConfig
+from .ops import BF16, Ctx
+from .taesd import TAESDHIP
+from .unet import UNetHIP
+
+EPSILON = 1e-7                                   # marigold_dc.py:20
+SUPPORTED_LOSS_FUNCS = ["l1", "l2", "edge", "smooth"]   # marigold_dc.py:19
+_NORM = {"const": 0, "minmax": 1, "percentile": 2}
+_PROJ = {"linear": 0, "log": 1, "log10": 2}
+
+
+class DDIMTables:
+    """DDIMScheduler(scaled_linear 0.00085..0.012, v_prediction, set_alpha_to_one=False,
+    timestep_spacing="trailing") reduced to per-step scalar tables (fp32, computed as the
+    scheduler does on the CPU)."""
+
+    def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012):
+        self.T = num_train_timesteps
+        betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, self.T, dtype=torch.float32) ** 2
+        self.alphas_cumprod = torch.cumprod(1.0 - betas, dim=0)
+        self.final_alpha_cumprod = self.alphas_cumprod[0]
+
+    def timesteps(self, steps: int) -> torch.Tensor:
+        ratio = self.T / steps
+        ts = np.round(np.arange(self.T, 0, -ratio)).astype(np.int64) - 1
+        return torch.from_numpy(ts)
+
+    def coef(self, steps: int) -> torch.Tensor:
+        rows = []
+        for t in self.timesteps(steps):
+            a = self.alphas_cumprod[t]
+            prev = int(t) - self.T // steps
+            ap = self.alphas_cumprod[prev] if prev >= 0 else self.final_alpha_cumprod
+            b = 1 - a
+            std = 0.0 * ((1 - ap) / b * (1 - a / ap)) ** 0.5
+            rows.append(torch.stack([a ** 0.5, b ** 0.5, ap ** 0.5, (1 - ap - std ** 2) ** 0.5]))
+        return torch.stack(rows).float()
+
+
+def adam_table(steps: int, lr_latent: float, lr_scaling: float, beta1=0.9, beta2=0.999) -> torch.Tensor:
+    """torch.optim.Adam scalars per step (Python doubles, cast to fp32 as the foreach kernels do)."""
+    rows = []
+    for k in range(1, steps + 1):
+        bc1 = 1 - beta1 ** k
+        bc2 = 1 - beta2 ** k
+        rows.append([lr_latent / bc1, bc2 ** 0.5, lr_scaling / bc1, 0.0])
+    return torch.tensor(rows, dtype=torch.float32)
+
+
+class MarigoldDepthCompletionPipeline:
+    """Guided-diffusion depth completion (Marigold-DC) on MI355X."""
+
+    def __init__(self, unet_state: dict, vae_state: dict, text_embedding: torch.Tensor,
+                 unet_config: UNetConfig = MARIGOLD_V1, device="cuda", use_graph: bool = True):
+        _lib.load()  # fail loudly without the HIP extension
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("MarigoldDepthCompletionPipeline (HIP) needs a GPU device")
+        self.dtype = BF16
+        self.ctx = Ctx(self.device)
+        self.unet = UNetHIP(unet_state, unet_config, self.device, text_embedding)
+        self.vae = TAESDHIP(vae_state, self.device)
+        self.scheduler = DDIMTables()
+        self.empty_text_embedding = text_embedding
+        self.use_graph = use_graph
+        self._plans = {}
+        self.last_loss = None
+
+    # ------------------------------------------------------------------ plans
+    def _plan(self, nb, h, w):
+        key = (nb, h, w)
+        if key not in self._plans:
+            up = self.unet.plan(self.ctx, nb, h, w)
+            dp = self.vae.decoder_plan(self.ctx, nb, h, w)
+            P = nb * h * w
+            st = {
+                "unet": up, "dec": dp, "graph": None, "graph_key": None,
+                "x0": torch.zeros(P, 8, dtype=BF16, device=self.device),
+                "gdir": torch.zeros(P, 8, dtype=BF16, device=self.device),
+                "eps_norm": torch.zeros(nb, dtype=torch.float32, device=self.device),
+                "m_lat": torch.zeros(P * 4, dtype=BF16, device=self.device),
+                "v_lat": torch.zeros(P * 4, dtype=BF16, device=self.device),
+                "affine": torch.zeros(nb, 2, dtype=torch.float32, device=self.device),
+                "m_aff": torch.zeros(nb, 2, dtype=torch.float32, device=self.device),
+                "v_aff": torch.zeros(nb, 2, dtype=torch.float32, device=self.device),
+                "daff": torch.zeros(nb, 2, dtype=torch.float32, device=self.device),
+                "loss": torch.zeros(nb, dtype=torch.float32, device=self.device),
+                "dbg": torch.zeros(nb, 4, dtype=torch.float32, device=self.device),
+                "dA": torch.zeros(nb, dp.H * dp.W, dtype=torch.float32, device=self.device),
+            }
+            self._plans[key] = st
+        return self._plans[key]
+
+    # ------------------------------------------------------------------ validation
+    @staticmethod
+    def _validate(imgs, sparses, pred_latents_prev, closed_form, train_latents, train_method, train_steps, beta,
+                  norm, percentile, projection, inv, min_depth, loss_funcs, resolution):
+        """marigold_dc.py:583-656 (same messages)."""
+        if (imgs.ndim != 4 or sparses.ndim != 4 or imgs.shape[0] != sparses.shape[0]
+                or imgs.shape[-2:] != sparses.shape[-2:]):
+            raise ValueError("Shape of image must be [N, C, H, W] and shape of sparse must be "
+                             f"[N, 1, H, W], but got image.shape: {imgs.shape} and sparse.shape: {sparses.shape}")
+        n, _, h, w = imgs.shape
+        # latent dims of the padded preprocessing size (equal to the reference's EH/EW whenever the
+        # reference itself runs; see module docstring)
+        eh = -(-(resolution * h // max(h, w)) // 8)
+        ew = -(-(resolution * w // max(h, w)) // 8)
+        if pred_latents_prev is not None:
+            if pred_latents_prev.ndim != 4 or tuple(pred_latents_prev.shape) != (n, 4, eh, ew):
+                raise ValueError(f"Shape of pred_latents_prev must be [N, 4, EH, EW], but got {pred_latents_prev.shape}")
+        if closed_form is None:
+            closed_form = not train_latents
+        elif not closed_form and not train_latents:
+            raise ValueError("Closed form solution must be enabled when trainable latents are not used. Set "
+                             "closed_form=True when train_latents=False, or just leave closed_form=None")
+        if train_method not in ["per-step", "per-input"]:
+            raise ValueError(f"Unknown train_method: {train_method}")
+        if train_method == "per-input" and train_steps <= 0:
+            raise ValueError("train_steps must be > 0 when per-input training is enabled")
+        if not (0 < beta < 1):
+            raise ValueError(f"beta must be in (0, 1), but got {beta}")
+        if norm == "percentile" and not all(0 <= p <= 1 for p in percentile):
+            raise ValueError(f"percentile must be in [0, 1], but got {percentile}")
+        if projection not in ["linear", "log", "log10"]:
+            raise ValueError(f"Unknown projection method: {projection}")
+        if (projection in ["log", "log10"] or inv) and min_depth <= EPSILON:
+            raise ValueError(f"min_depth must be > {EPSILON} when projection is 'log' or 'log10' or inv is True, "
+                             f"but got {min_depth}")
+        if loss_funcs is not None:
+            for f in loss_funcs:
+                if f not in SUPPORTED_LOSS_FUNCS:
+                    raise ValueError(f"Unknown loss function: {f}")
+        if norm not in _NORM:
+            raise ValueError(f"Unknown norm method: {norm}")
+        return closed_form
+
+    # ------------------------------------------------------------------ call
+    def __call__(self, imgs, sparses, max_depth, min_depth=0.0, projection="linear", inv=False, norm="minmax",
+                 percentile=(0.01, 0.99), pred_latents_prev=None, beta=0.9, steps=50, resolution=768,
+                 closed_form=None, opt="adam", lr=None, kld=False, kld_weight=0.1, kld_mode="simple",
+                 interp_mode="bilinear", loss_funcs=None, seed=2024, train_latents=True, train_method="per-step",
+                 train_steps=10, init_noise=None):
+        closed_form = self._validate(imgs, sparses, pred_latents_prev, closed_form, train_latents, train_method,
+                                     train_steps, beta, norm, percentile, projection, inv, min_depth, loss_funcs,
+                                     resolution)
+        if opt not in ("adam", "sgd", "adagrad"):
+            raise ValueError(f"Unknown optimizer: {opt}")
+        lr_latent, lr_scaling = (0.05, 0.005) if lr is None else lr
+        loss_funcs = ["l1", "l2"] if loss_funcs is None else list(loss_funcs)
+        # the hot path of this build (SURVEY.md §8 defaults); other modes are §8(f) "next" rows
+        unsupported = []
+        if closed_form or not train_latents:
+            unsupported.append("closed_form / train_latents=False")
+        if train_method != "per-step":
+            unsupported.append("train_method=per-input")
+        if opt != "adam":
+            unsupported.append(f"opt={opt}")
+        if kld:
+            unsupported.append("kld")
+        if sorted(loss_funcs) != ["l1", "l2"]:
+            unsupported.append(f"loss_funcs={loss_funcs}")
+        if interp_mode != "bilinear":
+            unsupported.append(f"interp_mode={interp_mode}")
+        if unsupported:
+            raise NotImplementedError("HIP path supports the predict.py default guided mode only; got "
+                                      + ", ".join(unsupported))
+        dev = self.device
+        ctx = self.ctx
+        imgs = imgs.to(dev)
+        sparses = sparses.to(dev, torch.float32).contiguous()
+        if imgs.dtype != torch.uint8:
+            raise ValueError("imgs must be uint8 [N, 3, H, W]")
+        n, _, H, W = imgs.shape
+        m = max(H, W)
+        RH, RW = H * resolution // m, W * resolution // m
+        PH, PW = -(-RH // 8) * 8, -(-RW // 8) * 8
+        h, w = PH // 8, PW // 8
+        st = self._plan(n, h, w)
+        up, dp = st["unet"], st["dec"]
+        P = n * h * w
+
+        # ---- initial latents (marigold_dc.py:661, 677-704)
+        gen = torch.Generator().manual_seed(seed)
+        noise = torch.randn((1, 4, h, w), generator=gen, dtype=BF16) if init_noise is None else init_noise
+        noise = noise.to(dev, BF16).contiguous()
+        prev = None
+        if pred_latents_prev is not None:
+            prev = pred_latents_prev.to(dev, BF16).contiguous()
+        _lib.call("dc_latent_init", noise.data_ptr(), ops.P(prev), float(beta), n, h * w, up.x8.data_ptr(),
+                  ctx.stream)
+
+        # ---- image latents (marigold_dc.py:687-698): preprocess + TAESD encoder into x8[..., 0:4]
+        img8 = torch.empty(n * PH * PW, 8, dtype=BF16, device=dev)
+        _lib.call("dc_preprocess_image", imgs.contiguous().data_ptr(), n, H, W, RH, RW, PH, PW, 1, img8.data_ptr(),
+                  ctx.stream)
+        self.vae.encode(ctx, img8, n, PH, PW, ops.Slice(up.x8, 0))
+        del img8
+
+        # ---- sparse guides (marigold_dc.py:706-756)
+        HWs = H * W
+        idx = torch.empty(n, HWs, dtype=torch.int32, device=dev)
+        gval = torch.empty(n, HWs, dtype=torch.float32, device=dev)
+        cnt = torch.empty(n, dtype=torch.int32, device=dev)
+        params = torch.empty(n, 8, dtype=torch.float32, device=dev)
+        lohi = None
+        if norm == "percentile":
+            # torch.quantile over the masked values (setup, once per call; marigold_dc.py:714-726)
+            q = torch.tensor(percentile, dtype=torch.float32)
+            sp_cpu = sparses.cpu()
+            lohi = torch.stack([torch.quantile(s[s > 0], q) for s in sp_cpu]).to(dev).contiguous()
+        _lib.call("dc_sparse_setup", sparses.data_ptr(), n, H, W, _NORM[norm], float(min_depth), float(max_depth),
+                  ops.P(lohi), _PROJ[projection], int(inv), idx.data_ptr(), gval.data_ptr(), cnt.data_ptr(),
+                  params.data_ptr(), ctx.stream)
+        cnt_host = cnt.cpu()
+        if (cnt_host == 0).any():
+            raise ValueError("No valid values found in mask for some positions. "
+                             "Ensure that mask has at least one True value along the specified dimensions.")
+        if projection != "linear" or inv:
+            raise NotImplementedError("non-linear depth space in the loss is a next-round row (SURVEY §8f)")
+
+        # ---- per-call tables
+        ts = self.scheduler.timesteps(steps)
+        coef = self.scheduler.coef(steps).to(dev)
+        adam = adam_table(steps, lr_latent, lr_scaling).to(dev)
+        self.unet.build_temb_tables(ctx, ts)
+        for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"]):
+            ops.memset(ctx, t)
+        st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))
+        ops.memset(ctx, ctx.step)
+        self._call_state = dict(idx=idx, gval=gval, cnt=cnt, params=params, coef=coef, adam=adam, H=H, W=W, RH=RH,
+                                RW=RW, PH=PH, PW=PW, n=n, h=h, w=w)
+
+        # ---- guided denoising loop (marigold_dc.py:800-904)
+        if self.use_graph:
+            g = st["graph"]
+            gkey = (steps, H, W, RH, RW, lr_latent, lr_scaling)
+            if g is None or st["graph_key"] != gkey:
+                # tables are rebuilt per call at new addresses: capture against this call's buffers
+                g = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize(dev)
+                s = torch.cuda.Stream(dev)
+                s.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(s):
+                    self._step(st)      # warm-up on a side stream (first-use lazy init)
+                torch.cuda.current_stream(dev).wait_stream(s)
+                torch.cuda.synchronize(dev)
+                # undo the warm-up step's state change
+                self._reset_state(st, n, noise, prev, beta)
+                with torch.cuda.graph(g):
+                    self._step(st)
+                st["graph"], st["graph_key"] = g, gkey
+                st["graph_tables"] = (coef, adam, idx, gval, cnt, params)
+            else:
+                # replay reads the captured table addresses: refresh their contents in place
+                old = st["graph_tables"]
+                for dst, src in zip(old, (coef, adam, idx, gval, cnt, params)):
+                    dst.copy_(src)
+            for _ in range(steps):
+                g.replay()
+        else:
+            for _ in range(steps):
+                self._step(st)
+
+        # ---- final decode (marigold_dc.py:969-985)
+        _lib.call("dc_taesd_clamp_fwd", ops.P(ops.Slice(up.x8, 4)), 8, P, dp.tin.data_ptr(), ctx.stream)
+        dp.forward()
+        dense = torch.empty(n, 1, H, W, dtype=torch.float32, device=dev)
+        cs = self._tables(st)
+        _lib.call("dc_final_dense", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["params"].data_ptr(),
+                  st["affine"].data_ptr(), dense.data_ptr(), ctx.stream)
+        lat = torch.empty(n, 4, h, w, dtype=BF16, device=dev)
+        _lib.call("dc_nhwc_to_nchw", ops.P(ops.Slice(up.x8, 4)), 8, n, h * w, 4, lat.data_ptr(), ctx.stream)
+        self.last_loss = st["loss"]
+        return dense, lat
+
+    def _tables(self, st):
+        cs = self._call_state
+        if self.use_graph and st.get("graph_tables") is not None:
+            coef, adam, idx, gval, cnt, params = st["graph_tables"]
+            return dict(cs, coef=coef, adam=adam, idx=idx, gval=gval, cnt=cnt, params=params)
+        return cs
+
+    def _reset_state(self, st, n, noise, prev, beta):
+        ctx = self.ctx
+        up = st["unet"]
+        _lib.call("dc_latent_init", noise.data_ptr(), ops.P(prev), float(beta), n, up.h * up.w, up.x8.data_ptr(),
+                  ctx.stream)
+        for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"]):
+            ops.memset(ctx, t)
+        st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))
+        ops.memset(ctx, ctx.step)
+
+    def _step(self, st):
+        """One guided DDIM step (marigold_dc.py:802-904) as a flat launch sequence."""
+        ctx = self.ctx
+        cs = self._tables(st)
+        up, dp = st["unet"], st["dec"]
+        n, h, w = cs["n"], cs["h"], cs["w"]
+        P = n * h * w
+        s = ctx.stream
+        step = ctx.step.data_ptr()
+        up.forward()                                                         # v = unet(cat(img, x_t), t)
+        _lib.call("dc_preview", up.x8.data_ptr(), up.v.data_ptr(), n, h * w, cs["coef"].data_ptr(), step,
+                  st["x0"].data_ptr(), dp.tin.data_ptr(), st["eps_norm"].data_ptr(), s)
+        dp.forward()                                                         # TAESD decode of x0
+        ops.memset(ctx, st["dA"])
+        _lib.call("dc_sparse_loss", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"], cs["W"],
+                  cs["idx"].data_ptr(), cs["gval"].data_ptr(), cs["cnt"].data_ptr(), cs["params"].data_ptr(),
+                  st["affine"].data_ptr(), st["dA"].data_ptr(), st["daff"].data_ptr(), st["loss"].data_ptr(), s)
+        _lib.call("dc_decode_tail_bwd", dp.out.data_ptr(), 8, st["dA"].data_ptr(), n, cs["PH"], cs["PW"], cs["RH"],
+                  cs["RW"], dp.dout.data_ptr(), s)
+        dp.backward()                                                        # d tin
+        _lib.call("dc_taesd_clamp_bwd", st["x0"].data_ptr(), 8, dp.dtin.data_ptr(), 8, P, cs["coef"].data_ptr(), step,
+                  st["gdir"].data_ptr(), up.dv.data_ptr(), s)
+        up.backward()                                                        # d x_t through the UNet
+        _lib.call("dc_latent_update", up.x8.data_ptr(), up.v.data_ptr(), st["gdir"].data_ptr(), up.gx.data_ptr(), n,
+                  h * w, cs["coef"].data_ptr(), cs["adam"].data_ptr(), step, st["eps_norm"].data_ptr(),
+                  st["m_lat"].data_ptr(), st["v_lat"].data_ptr(), st["affine"].data_ptr(), st["m_aff"].data_ptr(),
+                  st["v_aff"].data_ptr(), st["daff"].data_ptr(), st["dbg"].data_ptr(), s)
+        _lib.call("dc_step_advance", step, s)

@@ -1,0 +1,490 @@
+"""UNet2DConditionModel (Marigold v1-0, SD2 architecture) forward + input-gradient on HIP kernels.
+
+Replaces ``self.unet(...)`` in ``_predict_noise`` (marigold_dc.py:459-465) and the UNet part of
+``losses.backward`` (marigold_dc.py:877).  A ``UNetPlan`` is built once per (frames, latent h, w):
+all activations, saved tensors and gradient buffers are allocated up front (NHWC pixel rows), and
+the forward / backward are flat lists of kernel launches with bound pointers -- the shape a
+hipGraph capture of one guided step needs.  Only the gradient w.r.t. the depth-latent half of the
+8-channel input is produced (the image-latent half and all weights are constants).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+from .config import UNetConfig
+from .ops import BF16, Ctx, Slice
+from .weights import Conv, Linear, Norm, fold_cross_attention, round_bf16
+
+
+class ResnetW:
+    def __init__(self, sd, pre, dev):
+        self.norm1 = Norm(sd[pre + "norm1.weight"], sd[pre + "norm1.bias"], dev, 1e-5)
+        self.conv1 = Conv(sd[pre + "conv1.weight"], sd[pre + "conv1.bias"], dev)
+        self.temb_w = sd[pre + "time_emb_proj.weight"]
+        self.temb_b = sd[pre + "time_emb_proj.bias"]
+        self.temb = Linear(self.temb_w, self.temb_b, dev, dgrad=False)
+        self.norm2 = Norm(sd[pre + "norm2.weight"], sd[pre + "norm2.bias"], dev, 1e-5)
+        self.conv2 = Conv(sd[pre + "conv2.weight"], sd[pre + "conv2.bias"], dev)
+        self.cin = self.conv1.cin
+        self.cout = self.conv1.cout
+        self.shortcut = None
+        if pre + "conv_shortcut.weight" in sd:
+            self.shortcut = Conv(sd[pre + "conv_shortcut.weight"], sd[pre + "conv_shortcut.bias"], dev)
+        self.temb_table = None  # [S][cout] bf16, per call
+
+
+class TransformerW:
+    def __init__(self, sd, pre, dev, heads, ctx):
+        self.heads = heads
+        self.norm = Norm(sd[pre + "norm.weight"], sd[pre + "norm.bias"], dev, 1e-6)
+        self.proj_in = Linear(sd[pre + "proj_in.weight"], sd[pre + "proj_in.bias"], dev)
+        self.proj_out = Linear(sd[pre + "proj_out.weight"], sd[pre + "proj_out.bias"], dev)
+        b = pre + "transformer_blocks.0."
+        self.ln1 = Norm(sd[b + "norm1.weight"], sd[b + "norm1.bias"], dev, 1e-5)
+        self.ln2 = Norm(sd[b + "norm2.weight"], sd[b + "norm2.bias"], dev, 1e-5)
+        self.ln3 = Norm(sd[b + "norm3.weight"], sd[b + "norm3.bias"], dev, 1e-5)
+        wqkv = torch.cat([sd[b + "attn1.to_q.weight"], sd[b + "attn1.to_k.weight"], sd[b + "attn1.to_v.weight"]], 0)
+        self.qkv = Linear(wqkv, None, dev)
+        self.out = Linear(sd[b + "attn1.to_out.0.weight"], sd[b + "attn1.to_out.0.bias"], dev)
+        U, D, c0 = fold_cross_attention(sd, b + "attn2.", ctx, heads)
+        self.U, self.D, self.c0 = U.to(dev), D.to(dev), c0.to(dev)
+        self.ff1 = Linear(sd[b + "ff.net.0.proj.weight"], sd[b + "ff.net.0.proj.bias"], dev)
+        self.ff2 = Linear(sd[b + "ff.net.2.weight"], sd[b + "ff.net.2.bias"], dev)
+        self.c = self.proj_in.cout
+
+
+def timestep_embedding(timesteps: torch.Tensor, dim: int) -> torch.Tensor:
+    """diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), fp32, host."""
+    half = dim // 2
+    exponent = -math.log(10000) * torch.arange(0, half, dtype=torch.float32) / half
+    emb = timesteps[:, None].float() * torch.exp(exponent)[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    return torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+
+
+class UNetHIP:
+    def __init__(self, sd: dict, cfg: UNetConfig, device, text_embedding: torch.Tensor):
+        dev = torch.device(device)
+        self.cfg = cfg
+        self.device = dev
+        ctx = text_embedding.reshape(-1, text_embedding.shape[-1]).float()
+        # conv_in: 8 input channels; input-gradient only for channels 4..7 (the depth latent)
+        self.conv_in = Conv(sd["conv_in.weight"], sd["conv_in.bias"], dev, dgrad_rows=[4, 5, 6, 7])
+        self.t_lin1 = Linear(sd["time_embedding.linear_1.weight"], sd["time_embedding.linear_1.bias"], dev, False)
+        self.t_lin2 = Linear(sd["time_embedding.linear_2.weight"], sd["time_embedding.linear_2.bias"], dev, False)
+        self.down = []
+        nb_ = len(cfg.block_out_channels)
+        for i in range(nb_):
+            blk = {"resnets": [], "attns": [], "down": None}
+            for j in range(cfg.layers_per_block):
+                blk["resnets"].append(ResnetW(sd, f"down_blocks.{i}.resnets.{j}.", dev))
+                if cfg.down_attn[i]:
+                    blk["attns"].append(TransformerW(sd, f"down_blocks.{i}.attentions.{j}.", dev, cfg.heads[i], ctx))
+            if i < nb_ - 1:
+                blk["down"] = Conv(sd[f"down_blocks.{i}.downsamplers.0.conv.weight"],
+                                   sd[f"down_blocks.{i}.downsamplers.0.conv.bias"], dev, stride=2)
+            self.down.append(blk)
+        self.mid_res = [ResnetW(sd, f"mid_block.resnets.{j}.", dev) for j in range(2)]
+        self.mid_attn = TransformerW(sd, "mid_block.attentions.0.", dev, cfg.heads[-1], ctx)
+        self.up = []
+        rev_heads = list(reversed(cfg.heads))
+        for i in range(nb_):
+            blk = {"resnets": [], "attns": [], "up": None}
+            for j in range(cfg.layers_per_block + 1):
+                blk["resnets"].append(ResnetW(sd, f"up_blocks.{i}.resnets.{j}.", dev))
+                if cfg.up_attn[i]:
+                    blk["attns"].append(TransformerW(sd, f"up_blocks.{i}.attentions.{j}.", dev, rev_heads[i], ctx))
+            if i < nb_ - 1:
+                blk["up"] = Conv(sd[f"up_blocks.{i}.upsamplers.0.conv.weight"],
+                                 sd[f"up_blocks.{i}.upsamplers.0.conv.bias"], dev)
+            self.up.append(blk)
+        self.norm_out = Norm(sd["conv_norm_out.weight"], sd["conv_norm_out.bias"], dev, 1e-5)
+        # conv_out 320->4: forward output padded to ld 8; input-gradient reads dv [P][8] (4..7 zero)
+        self.conv_out = Conv(sd["conv_out.weight"], sd["conv_out.bias"], dev, dgrad_cout_pad=8)
+
+    def resnets(self):
+        for blk in self.down:
+            yield from blk["resnets"]
+        yield from self.mid_res
+        for blk in self.up:
+            yield from blk["resnets"]
+
+    def build_temb_tables(self, ctx: Ctx, timesteps: torch.Tensor):
+        """Per-resnet time-embedding projections for every timestep of the call: [S][cout] bf16.
+
+        diffusers: t_emb (fp32) -> bf16 -> linear_1 -> SiLU -> linear_2 (= emb); each resnet adds
+        time_emb_proj(SiLU(emb)) to conv1's output (ResnetBlock2D).  Run on the device kernels.
+        """
+        S = timesteps.shape[0]
+        c0 = self.cfg.block_out_channels[0]
+        te = timestep_embedding(timesteps.cpu(), c0).to(BF16).to(self.device)
+        d = self.cfg.time_embed_dim
+        h1 = torch.empty(S, d, dtype=BF16, device=self.device)
+        ops.linear(ctx, te, self.t_lin1.wf, S, d, h1, bias=self.t_lin1.bias)
+        a1 = torch.empty_like(h1)
+        ops.silu(ctx, h1, a1)
+        emb = torch.empty_like(h1)
+        ops.linear(ctx, a1, self.t_lin2.wf, S, d, emb, bias=self.t_lin2.bias)
+        semb = torch.empty_like(emb)
+        ops.silu(ctx, emb, semb)
+        for r in self.resnets():
+            # tables keep their address across calls with the same step count (hipGraph replay)
+            if r.temb_table is None or r.temb_table.shape[0] != S:
+                r.temb_table = torch.empty(S, r.cout, dtype=BF16, device=self.device)
+            ops.linear(ctx, semb, r.temb.wf, S, r.cout, r.temb_table, bias=r.temb.bias)
+
+    def plan(self, ctx: Ctx, nb: int, h: int, w: int) -> "UNetPlan":
+        return UNetPlan(self, ctx, nb, h, w)
+
+
+def _conv_out_hw(h, stride):
+    return (h + 2 - 3) // stride + 1
+
+
+class UNetPlan:
+    """Buffers + launch lists for one (frames, h, w).  ``x8`` [P][8]: image latents (0..3) and depth
+    latents (4..7); ``v`` [P][8]: the v-prediction (0..3); ``dv`` [P][8]: its incoming gradient;
+    ``gx`` [P][8]: gradient w.r.t. the depth latents (0..3)."""
+
+    def __init__(self, net: UNetHIP, ctx: Ctx, nb: int, h: int, w: int):
+        self.net, self.ctx, self.nb, self.h, self.w = net, ctx, nb, h, w
+        dev = net.device
+        self.dev = dev
+        self.fwd: list = []
+        self.tape: list = []          # (kind, info) in forward order
+        self.saved: list = []         # keep-alive for every buffer
+        P = nb * h * w
+        self.x8 = self.buf(P, 8)
+        self.v = self.buf(P, 8)
+        self.dv = self.buf(P, 8)
+        self.gx = self.buf(P, 8)
+        self._build_forward()
+        self.bwd: list = []
+        self._build_backward()
+
+    # ------------------------------------------------------------------ helpers
+    def buf(self, rows, cols, dtype=BF16):
+        t = torch.zeros(rows, cols, dtype=dtype, device=self.dev)
+        self.saved.append(t)
+        return t
+
+    def fbuf(self, *shape):
+        t = torch.zeros(*shape, dtype=torch.float32, device=self.dev)
+        self.saved.append(t)
+        return t
+
+    # ------------------------------------------------------------------ forward
+    def _resnet(self, r: ResnetW, x, hw, x2=None, c1=0):
+        ctx, nb = self.ctx, self.nb
+        hh, ww = hw
+        P = nb * hh * ww
+        cin, cout = r.cin, r.cout
+        g1 = self.buf(P, cin)
+        st1 = self.fbuf(nb, 32, 2)
+        h1 = self.buf(P, cout)
+        st2 = self.fbuf(nb, 32, 2)
+        g2 = self.buf(P, cout)
+        out = self.buf(P, cout)
+        sc = self.buf(P, cout) if r.shortcut is not None else None
+
+        def f():
+            ops.groupnorm(ctx, x, nb, hh * ww, cin, r.norm1.gamma, r.norm1.beta, r.norm1.eps, True, g1, st1, x2=x2,
+                          c1=c1)
+            ops.conv_gemm(ctx, g1, r.conv1.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
+                          bias=r.conv1.bias, rowbias=r.temb_table, rowbias_ld=cout, y=h1)
+            ops.groupnorm(ctx, h1, nb, hh * ww, cout, r.norm2.gamma, r.norm2.beta, r.norm2.eps, True, g2, st2)
+            res = x
+            if r.shortcut is not None:
+                ops.conv_gemm(ctx, x, r.shortcut.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
+                              kh=1, kw=1, pad=0, x2=x2, c1=c1, bias=r.shortcut.bias, y=sc)
+                res = sc
+            ops.conv_gemm(ctx, g2, r.conv2.wf, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout,
+                          bias=r.conv2.bias, resid=res, y=out)
+
+        self.fwd.append(f)
+        self.tape.append(("resnet", dict(r=r, x=x, x2=x2, c1=c1, hw=hw, st1=st1, h1=h1, st2=st2, out=out)))
+        return out
+
+    def _transformer(self, t: TransformerW, x, hw):
+        ctx, nb = self.ctx, self.nb
+        hh, ww = hw
+        T = hh * ww
+        P = nb * T
+        C, H = t.c, t.heads
+        n0 = self.buf(P, C)
+        st0 = self.fbuf(nb, 32, 2)
+        p = self.buf(P, C)
+        l1 = self.buf(P, C)
+        sl1 = self.fbuf(P, 2)
+        qkv = self.buf(P, 3 * C)
+        o = self.buf(P, C)
+        lse = self.fbuf(nb, H, T)
+        r1 = self.buf(P, C)
+        r2 = self.buf(P, C)
+        sl2 = self.fbuf(P, 2)
+        probs = self.fbuf(P, H)
+        l3 = self.buf(P, C)
+        sl3 = self.fbuf(P, 2)
+        f8 = self.buf(P, 8 * C)
+        gg = self.buf(P, 4 * C)
+        r3 = self.buf(P, C)
+        out = self.buf(P, C)
+
+        def f():
+            ops.groupnorm(ctx, x, nb, T, C, t.norm.gamma, t.norm.beta, t.norm.eps, False, n0, st0)
+            ops.linear(ctx, n0, t.proj_in.wf, P, C, p, bias=t.proj_in.bias)
+            ops.layernorm(ctx, p, P, C, t.ln1.gamma, t.ln1.beta, t.ln1.eps, l1, sl1)
+            ops.linear(ctx, l1, t.qkv.wf, P, 3 * C, qkv)
+            ops.attn_fwd(ctx, qkv, nb, T, H, o, lse)
+            ops.linear(ctx, o, t.out.wf, P, C, r1, bias=t.out.bias, resid=p)
+            ops.crossattn_fwd(ctx, r1, P, C, H, t.ln2.eps, t.ln2.gamma, t.ln2.beta, t.U, t.D, t.c0, r2, sl2, probs)
+            ops.layernorm(ctx, r2, P, C, t.ln3.gamma, t.ln3.beta, t.ln3.eps, l3, sl3)
+            ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias)
+            ops.geglu(ctx, f8, P, 4 * C, gg)
+            ops.linear(ctx, gg, t.ff2.wf, P, C, r3, bias=t.ff2.bias, resid=r2)
+            ops.linear(ctx, r3, t.proj_out.wf, P, C, out, bias=t.proj_out.bias, resid=x)
+
+        self.fwd.append(f)
+        self.tape.append(("transformer", dict(t=t, x=x, hw=hw, st0=st0, p=p, sl1=sl1, qkv=qkv, o=o, lse=lse, r1=r1,
+                                              r2=r2, sl2=sl2, probs=probs, sl3=sl3, f8=f8, out=out)))
+        return out
+
+    def _downsample(self, cv: Conv, x, hw):
+        ctx, nb = self.ctx, self.nb
+        hh, ww = hw
+        ho, wo = _conv_out_hw(hh, 2), _conv_out_hw(ww, 2)
+        out = self.buf(nb * ho * wo, cv.cout)
+
+        def f():
+            ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, stride=2,
+                          bias=cv.bias, y=out)
+
+        self.fwd.append(f)
+        self.tape.append(("down", dict(cv=cv, x=x, hw=hw, ohw=(ho, wo), out=out)))
+        return out, (ho, wo)
+
+    def _upsample(self, cv: Conv, x, hw, ohw):
+        ctx, nb = self.ctx, self.nb
+        hh, ww = hw
+        ho, wo = ohw
+        out = self.buf(nb * ho * wo, cv.cout)
+
+        def f():
+            ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, mode=1,
+                          bias=cv.bias, y=out)
+
+        self.fwd.append(f)
+        self.tape.append(("up", dict(cv=cv, x=x, hw=hw, ohw=ohw, out=out)))
+        return out
+
+    def _build_forward(self):
+        net, ctx, nb = self.net, self.ctx, self.nb
+        cfg = net.cfg
+        hw = (self.h, self.w)
+        c0 = cfg.block_out_channels[0]
+        h0 = self.buf(nb * self.h * self.w, c0)
+        x8 = self.x8
+
+        def f_in():
+            ops.conv_gemm(ctx, x8, net.conv_in.wf, nb=nb, hin=self.h, win=self.w, cin=8, hout=self.h, wout=self.w,
+                          cout=c0, bias=net.conv_in.bias, y=h0)
+
+        self.fwd.append(f_in)
+        self.tape.append(("conv_in", dict(out=h0)))
+        skips = [(h0, hw)]
+        x = h0
+        sizes = [hw]
+        for i, blk in enumerate(net.down):
+            for j, r in enumerate(blk["resnets"]):
+                x = self._resnet(r, x, hw)
+                if blk["attns"]:
+                    x = self._transformer(blk["attns"][j], x, hw)
+                skips.append((x, hw))
+            if blk["down"] is not None:
+                x, hw = self._downsample(blk["down"], x, hw)
+                skips.append((x, hw))
+                sizes.append(hw)
+        x = self._resnet(net.mid_res[0], x, hw)
+        x = self._transformer(net.mid_attn, x, hw)
+        x = self._resnet(net.mid_res[1], x, hw)
+        for i, blk in enumerate(net.up):
+            for j, r in enumerate(blk["resnets"]):
+                s, shw = skips.pop()
+                assert shw == hw
+                c1 = x.shape[1]
+                x = self._resnet(r, x, hw, x2=s, c1=c1)
+                if blk["attns"]:
+                    x = self._transformer(blk["attns"][j], x, hw)
+            if blk["up"] is not None:
+                ohw = skips[-1][1]  # diffusers forward_upsample_size: upsample to the next skip's size
+                x = self._upsample(blk["up"], x, hw, ohw)
+                hw = ohw
+        # head: GN + SiLU + conv_out
+        P = nb * self.h * self.w
+        g = self.buf(P, c0)
+        st = self.fbuf(nb, 32, 2)
+        xin = x
+
+        def f_out():
+            ops.groupnorm(ctx, xin, nb, self.h * self.w, c0, net.norm_out.gamma, net.norm_out.beta, net.norm_out.eps,
+                          True, g, st)
+            ops.conv_gemm(ctx, g, net.conv_out.wf, nb=nb, hin=self.h, win=self.w, cin=c0, hout=self.h, wout=self.w,
+                          cout=4, bias=net.conv_out.bias, y=self.v)
+
+        self.fwd.append(f_out)
+        self.tape.append(("head", dict(x=xin, st=st)))
+
+    # ------------------------------------------------------------------ backward
+    def _build_backward(self):
+        net, ctx, nb = self.net, self.ctx, self.nb
+        grad_of = {}   # id(tensor) -> grad tensor / Slice
+        extra_of = {}  # id(skip tensor) -> Slice of the up-resnet's concat gradient
+        dev_h, dev_w = self.h, self.w
+        bwd = []
+        for kind, d in reversed(self.tape):
+            if kind == "head":
+                x = d["x"]
+                P = nb * dev_h * dev_w
+                c0 = x.shape[1]
+                dg = self.buf(P, c0)
+                dx = self.buf(P, c0)
+                grad_of[id(x)] = dx
+                st = d["st"]
+
+                def b(x=x, dg=dg, dx=dx, st=st, c0=c0):
+                    ops.conv_gemm(ctx, self.dv, net.conv_out.wd, nb=nb, hin=dev_h, win=dev_w, cin=8, hout=dev_h,
+                                  wout=dev_w, cout=c0, y=dg)
+                    ops.groupnorm_bwd(ctx, x, nb, dev_h * dev_w, c0, net.norm_out.gamma, net.norm_out.beta, True,
+                                      st, dg, dx)
+
+                bwd.append(b)
+            elif kind == "up":
+                cv, x, (hh, ww), (ho, wo), out = d["cv"], d["x"], d["hw"], d["ohw"], d["out"]
+                dout = grad_of[id(out)]
+                dhi = self.buf(nb * ho * wo, cv.cin)
+                dx = self.buf(nb * hh * ww, cv.cin)
+                grad_of[id(x)] = dx
+
+                def b(cv=cv, dout=dout, dhi=dhi, dx=dx, hh=hh, ww=ww, ho=ho, wo=wo):
+                    ops.conv_gemm(ctx, dout, cv.wd, nb=nb, hin=ho, win=wo, cin=cv.cout, hout=ho, wout=wo,
+                                  cout=cv.cin, y=dhi)
+                    ops.upsample_adjoint(ctx, dhi, nb, ho, wo, cv.cin, hh, ww, dx)
+
+                bwd.append(b)
+            elif kind == "down":
+                cv, x, (hh, ww), (ho, wo), out = d["cv"], d["x"], d["hw"], d["ohw"], d["out"]
+                dout = grad_of[id(out)]
+                dx = self.buf(nb * hh * ww, cv.cin)
+                grad_of[id(x)] = dx
+                extra = extra_of.get(id(x))
+
+                def b(cv=cv, dout=dout, dx=dx, hh=hh, ww=ww, ho=ho, wo=wo, extra=extra):
+                    ops.conv_gemm(ctx, dout, cv.wd, nb=nb, hin=ho, win=wo, cin=cv.cout, hout=hh, wout=ww,
+                                  cout=cv.cin, mode=2, resid=extra, y=dx)
+
+                bwd.append(b)
+            elif kind == "transformer":
+                bwd.append(self._transformer_bwd(d, grad_of, extra_of))
+            elif kind == "resnet":
+                bwd.append(self._resnet_bwd(d, grad_of, extra_of))
+            elif kind == "conv_in":
+                out = d["out"]
+                dout = grad_of[id(out)]
+
+                def b(dout=dout):
+                    ops.conv_gemm(ctx, dout, net.conv_in.wd, nb=nb, hin=dev_h, win=dev_w, cin=net.conv_in.cout,
+                                  hout=dev_h, wout=dev_w, cout=4, y=self.gx)
+
+                bwd.append(b)
+        self.bwd = bwd
+
+    def _resnet_bwd(self, d, grad_of, extra_of):
+        ctx, nb = self.ctx, self.nb
+        r, x, x2, c1, (hh, ww) = d["r"], d["x"], d["x2"], d["c1"], d["hw"]
+        st1, h1, st2, out = d["st1"], d["h1"], d["st2"], d["out"]
+        P = nb * hh * ww
+        cin, cout = r.cin, r.cout
+        dout = grad_of[id(out)]
+        dg2 = self.buf(P, cout)
+        dh1 = self.buf(P, cout)
+        dg1 = self.buf(P, cin)
+        dx = self.buf(P, cin)
+        if x2 is not None:
+            grad_of[id(x)] = Slice(dx, 0)
+            extra_of[id(x2)] = Slice(dx, c1)
+            extra = None
+        else:
+            grad_of[id(x)] = dx
+            extra = extra_of.get(id(x))
+
+        def b():
+            ops.conv_gemm(ctx, dout, r.conv2.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout, y=dg2)
+            ops.groupnorm_bwd(ctx, h1, nb, hh * ww, cout, r.norm2.gamma, r.norm2.beta, True, st2, dg2, dh1)
+            ops.conv_gemm(ctx, dh1, r.conv1.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin, y=dg1)
+            if r.shortcut is None:
+                ops.groupnorm_bwd(ctx, x, nb, hh * ww, cin, r.norm1.gamma, r.norm1.beta, True, st1, dg1, dx,
+                                  x2=x2, c1=c1, add1=dout, add2=extra)
+            else:
+                ops.groupnorm_bwd(ctx, x, nb, hh * ww, cin, r.norm1.gamma, r.norm1.beta, True, st1, dg1, dx,
+                                  x2=x2, c1=c1, add1=extra)
+                ops.conv_gemm(ctx, dout, r.shortcut.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin,
+                              kh=1, kw=1, pad=0, resid=dx, y=dx)
+
+        return b
+
+    def _transformer_bwd(self, d, grad_of, extra_of):
+        ctx, nb = self.ctx, self.nb
+        t, x, (hh, ww) = d["t"], d["x"], d["hw"]
+        T = hh * ww
+        P = nb * T
+        C, H = t.c, t.heads
+        out = d["out"]
+        dout = grad_of[id(out)]
+        dr3 = self.buf(P, C)
+        dgg = self.buf(P, 4 * C)
+        df = self.buf(P, 8 * C)
+        dl3 = self.buf(P, C)
+        dr2 = self.buf(P, C)
+        dr1 = self.buf(P, C)
+        do = self.buf(P, C)
+        dqkv = self.buf(P, 3 * C)
+        dl1 = self.buf(P, C)
+        dp = self.buf(P, C)
+        dn0 = self.buf(P, C)
+        dx = self.buf(P, C)
+        delta = self.fbuf(nb, H, T)
+        grad_of[id(x)] = dx
+        extra = extra_of.get(id(x))
+        st0, p, sl1, qkv, o, lse = d["st0"], d["p"], d["sl1"], d["qkv"], d["o"], d["lse"]
+        r1, r2, sl2, probs, sl3, f8 = d["r1"], d["r2"], d["sl2"], d["probs"], d["sl3"], d["f8"]
+
+        def b():
+            ops.linear(ctx, dout, t.proj_out.wd, P, C, dr3)
+            ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, dgg)
+            ops.geglu_bwd(ctx, f8, P, 4 * C, dgg, df)
+            ops.linear(ctx, df, t.ff1.wd, P, C, dl3)
+            ops.layernorm_bwd(ctx, r2, P, C, t.ln3.gamma, sl3, dl3, dr2, add=dr3)
+            ops.crossattn_bwd(ctx, r1, P, C, H, t.ln2.gamma, t.U, t.D, sl2, probs, dr2, dr1)
+            ops.linear(ctx, dr1, t.out.wd, P, C, do)
+            ops.attn_bwd(ctx, qkv, o, do, lse, nb, T, H, delta, dqkv)
+            ops.linear(ctx, dqkv, t.qkv.wd, P, C, dl1)
+            ops.layernorm_bwd(ctx, p, P, C, t.ln1.gamma, sl1, dl1, dp, add=dr1)
+            ops.linear(ctx, dp, t.proj_in.wd, P, C, dn0)
+            ops.groupnorm_bwd(ctx, x, nb, T, C, t.norm.gamma, t.norm.beta, False, st0, dn0, dx, add1=dout,
+                              add2=extra)
+
+        return b
+
+    # ------------------------------------------------------------------ run
+    def forward(self):
+        for f in self.fwd:
+            f()
+        return self.v
+
+    def backward(self):
+        for b in self.bwd:
+            b()
+        return self.gx

@@ -1,0 +1,106 @@
+"""Weight packing: diffusers-format state dicts -> device layouts of the HIP kernels.
+
+* conv  [cout][cin][kh][kw]  -> forward  [cout][ktot]  K order (ky, kx, cin), cin padded to 8,
+                                ktot padded to 64 (dc_conv_desc contract)
+                             -> input-gradient W'[cin][ky][kx][cout] = W[cout][cin][kh-1-ky][kw-1-kx]
+* linear [out][in]           -> forward as-is, input-gradient = W^T
+* the folded 2-key cross-attention constants U, D, c0 (DESIGN.md "cross-attention")
+This is a one-time, load-time layout transform (like a checkpoint converter); nothing here runs per step.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+BF16 = torch.bfloat16
+
+
+def _pad_k(t: torch.Tensor) -> torch.Tensor:
+    k = t.shape[1]
+    kt = -(-k // 64) * 64
+    return F.pad(t, (0, kt - k)) if kt != k else t
+
+
+def pack_conv(w: torch.Tensor, cin_pad: int | None = None) -> torch.Tensor:
+    co, ci, kh, kw = w.shape
+    cp = cin_pad or ci
+    t = torch.zeros(co, kh, kw, cp, dtype=torch.float32)
+    t[..., :ci] = w.float().permute(0, 2, 3, 1)
+    return _pad_k(t.reshape(co, -1)).contiguous()
+
+
+def pack_conv_dgrad(w: torch.Tensor, rows=None, cout_pad: int | None = None) -> torch.Tensor:
+    wd = w.float().flip(2, 3).permute(1, 0, 2, 3)  # [cin][cout][kh][kw]
+    if rows is not None:
+        wd = wd[rows]
+    return pack_conv(wd, cin_pad=cout_pad)
+
+
+def round_bf16(t: torch.Tensor) -> torch.Tensor:
+    return t.to(BF16).float()
+
+
+class Conv:
+    """A conv with forward and input-gradient packings on the device."""
+
+    def __init__(self, w, b, device, *, stride=1, cin_pad=None, dgrad=True, dgrad_rows=None, dgrad_cout_pad=None):
+        w = round_bf16(w)  # the reference runs bf16 weights (predict.py:474-488, torch_dtype=bf16)
+        self.cout, self.cin, self.kh, self.kw = w.shape
+        self.stride = stride
+        self.pad = self.kh // 2
+        self.cin_p = cin_pad or self.cin
+        self.wf = pack_conv(w, cin_pad).to(device=device, dtype=BF16)
+        self.bias = b.float().to(BF16).float().to(device) if b is not None else None
+        self.wd = None
+        if dgrad:
+            self.dg_cout = len(dgrad_rows) if dgrad_rows is not None else self.cin
+            self.dg_cin_p = dgrad_cout_pad or self.cout
+            self.wd = pack_conv_dgrad(w, dgrad_rows, dgrad_cout_pad).to(device=device, dtype=BF16)
+
+
+class Linear:
+    def __init__(self, w, b, device, dgrad=True):
+        w = round_bf16(w)
+        self.cout, self.cin = w.shape
+        self.wf = w.contiguous().to(device=device, dtype=BF16)
+        self.bias = b.float().to(BF16).float().to(device) if b is not None else None
+        self.wd = w.t().contiguous().to(device=device, dtype=BF16) if dgrad else None
+
+
+class Norm:
+    def __init__(self, w, b, device, eps):
+        self.gamma = round_bf16(w).to(device)
+        self.beta = round_bf16(b).to(device)
+        self.eps = eps
+
+
+def fold_cross_attention(sd: dict, pre: str, ctx: torch.Tensor, heads: int):
+    """attn2 with a constant 2-token context -> (U [H][C], D [H][C], c0 [C]) in fp32.
+
+    softmax over 2 keys: p0 = sigmoid(q.(k0-k1)/sqrt(64)); out = v1 + p0 (v0 - v1) per head, so
+    attn2(n) = Wo(v1) + bo + sum_h p0_h Wo_h(v0_h - v1_h),  p0_h = sigmoid(n . U_h),
+    U_h = Wq_h^T (k0_h - k1_h) / 8,  D_h = Wo_h (v0_h - v1_h),  c0 = Wo v1 + bo.
+    k, v are rounded to bf16 as the reference computes them (to_k/to_v in bf16).
+    """
+    wq = round_bf16(sd[pre + "to_q.weight"]).double()
+    wk = round_bf16(sd[pre + "to_k.weight"]).double()
+    wv = round_bf16(sd[pre + "to_v.weight"]).double()
+    wo = round_bf16(sd[pre + "to_out.0.weight"]).double()
+    bo = round_bf16(sd[pre + "to_out.0.bias"]).double()
+    c = round_bf16(ctx).double()  # [2][cross]
+    k = round_bf16((c @ wk.t()).float()).double()  # [2][inner]
+    v = round_bf16((c @ wv.t()).float()).double()
+    inner = wq.shape[0]
+    hd = inner // heads
+    C = wq.shape[1]
+    U = torch.zeros(heads, C, dtype=torch.float64)
+    D = torch.zeros(heads, wo.shape[0], dtype=torch.float64)
+    scale = 1.0 / math.sqrt(hd)
+    for h in range(heads):
+        sl = slice(h * hd, (h + 1) * hd)
+        U[h] = wq[sl].t() @ (k[0, sl] - k[1, sl]) * scale
+        D[h] = wo[:, sl] @ (v[0, sl] - v[1, sl])
+    c0 = wo @ v[1] + bo
+    return U.float(), D.float(), c0.float()

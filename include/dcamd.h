@@ -1,0 +1,142 @@
+/*
+ * dcamd.h -- C ABI of the MI355X-native Marigold-DC guided sampler (libdcamd.so, gfx950).
+ *
+ * The reference (tier4/depth_completion) has no native/FFI boundary: its hot path is the Python
+ * operator API MarigoldDepthCompletionPipeline.__call__ (marigold_dc.py:467-985), executed by
+ * diffusers/PyTorch CUDA kernels.  This header is the boundary the MI355X build inserts beneath
+ * that API: plain device pointers, sizes and a hipStream_t (passed as void*), every entry point
+ * returning an int status (0 = ok, 1 = bad argument, 2 = launch failure, 3 = alignment).  No
+ * torch types cross it.  Layouts: bf16 tensors are NHWC "pixel rows" (row stride `ld*` in
+ * elements, multiple of 8); fp32 for statistics, affine parameters and losses.
+ *
+ * Which reference call each group replaces is noted per function.
+ */
+#ifndef DCAMD_H
+#define DCAMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int dc_abi_version(void);
+
+/* ---------------------------------------------------------------- matmul-shaped ops
+ * Implicit-GEMM conv / linear on MFMA.  Replaces the cuDNN conv fwd/dgrad and cuBLAS GEMMs that
+ * diffusers' UNet2DConditionModel (_predict_noise, marigold_dc.py:459-465) and AutoencoderTiny
+ * (decode_prediction, marigold_dc.py:366; prepare_latents, :696-698) launch, and their autograd
+ * input-gradients (losses.backward, marigold_dc.py:877).  Weight gradients are not computed: the
+ * reference optimizer only holds latents and affine parameters (marigold_dc.py:777-781).
+ * mode: 0 direct conv (stride/pad), 1 nearest-upsample hin->hout folded into the gather (Upsample2D),
+ *       2 transposed stride-2 gather (input-gradient of a stride-2 3x3 conv, Downsample2D).
+ * Epilogue order: acc + bias -> (+ rowbias[*rowbias_idx]) -> (+ resid) -> relu? -> (* [mask > 0]).
+ */
+typedef struct dc_conv_desc {
+  const void* x;   /* bf16 [nb*hin*win][ldx] */
+  const void* x2;  /* optional second source for channels >= c1 (skip concat) */
+  int ldx, ldx2, c1;
+  int nb, hin, win, cin;
+  int hout, wout;
+  int kh, kw, stride, pad, mode;
+  const void* w;   /* bf16 [cout][ktot], K order (ky, kx, cin), ktot % 64 == 0 */
+  int ktot, cout;
+  const float* bias;
+  const void* rowbias;
+  const int* rowbias_idx;
+  int rowbias_ld;
+  const void* resid;
+  int ldr;
+  const void* mask;
+  int ldmask;
+  int act;         /* 0 none, 1 relu */
+  void* y;
+  int ldy;
+  float* ws;       /* split-K workspace (may be NULL: no split-K) */
+  long long ws_bytes;
+} dc_conv_desc;
+
+int dc_conv_gemm(const dc_conv_desc* d, void* stream);
+
+/* ---------------------------------------------------------------- normalisation
+ * GroupNorm(+SiLU) fwd/bwd (ResnetBlock2D.norm1/norm2, Transformer2DModel.norm, conv_norm_out) and
+ * LayerNorm fwd/bwd (BasicTransformerBlock.norm1/norm3).  stats: [nb][groups][2] (mean, rstd).
+ */
+long long dc_groupnorm_ws_bytes(int nb, int hw, int c, int groups);
+int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c, int groups,
+                     float eps, const float* gamma, const float* beta, int silu, void* y, int ldy, float* stats,
+                     float* ws, void* stream);
+int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c, int groups,
+                     const float* gamma, const float* beta, int silu, const float* stats, const void* dy, int lddy,
+                     void* dx, int lddx, const void* add1, int ldadd1, const void* add2, int ldadd2, float* ws,
+                     void* stream);
+int dc_layernorm_fwd(const void* x, int ldx, long long rows, int c, float eps, const float* gamma, const float* beta,
+                     void* y, int ldy, float* stats, void* stream);
+int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, const float* gamma, const float* stats,
+                     const void* dy, int lddy, void* dx, int lddx, const void* add, int ldadd, void* stream);
+
+/* ---------------------------------------------------------------- attention (head dim 64)
+ * Self-attention (Attention.attn1 via SDPA) fwd/bwd and the folded 2-key cross-attention
+ * (attn2 with the constant empty-prompt context, marigold_dc.py:463, :663-674) fused with norm2.
+ */
+int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse, void* stream);
+int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, const void* dout, int lddo, const float* lse, int nb,
+                int t, int heads, float* delta_ws, void* dqkv, int ldd, void* stream);
+int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps, const float* gamma,
+                     const float* beta, const float* U, const float* D, const float* c0, void* y, int ldy,
+                     float* stats, float* probs, void* stream);
+int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, int heads, const float* gamma, const float* U,
+                     const float* D, const float* stats, const float* probs, const void* dy, int lddy, void* dx,
+                     int lddx, void* stream);
+
+/* ---------------------------------------------------------------- elementwise
+ * GEGLU (FeedForward.net[0]), nearest-upsample adjoint (Upsample2D / TAESD Upsample backward),
+ * TAESD DecoderTiny input clamp tanh(x/3)*3 and its backward fused with the Tweedie-preview
+ * backward, image preprocessing (MarigoldImageProcessor.preprocess, marigold_dc.py:687-692, plus
+ * EncoderTiny's x.add(1).div(2)), layout conversion at the API boundary.
+ */
+int dc_geglu_fwd(const void* f, int ldf, long long rows, int c, void* y, int ldy, void* stream);
+int dc_geglu_bwd(const void* f, int ldf, long long rows, int c, const void* dy, int lddy, void* df, int lddf,
+                 void* stream);
+int dc_upsample_adjoint(const void* dhi, int ldhi, int nb, int hhi, int whi, int c, int hlo, int wlo, void* dlo,
+                        int ldlo, const void* mask, int ldmask, void* stream);
+int dc_taesd_clamp_fwd(const void* x, int ldx, long long pixels, void* y, void* stream);
+int dc_taesd_clamp_bwd(const void* x0, int ldx0, const void* dy, int lddy, long long pixels, const float* coef,
+                       const int* step, void* gx_direct, void* dv, void* stream);
+int dc_silu(const void* x, long long n, void* y, void* stream);
+int dc_preprocess_image(const void* img_u8, int nb, int h, int w, int rh, int rw, int ph, int pw, int encoder_input,
+                        void* out, void* stream);
+int dc_nhwc_to_nchw(const void* x, int ldx, int nb, long long hw, int c, void* y, void* stream);
+int dc_nchw_to_nhwc(const void* x, int nb, long long hw, int c, void* y, int ldy, void* stream);
+
+/* ---------------------------------------------------------------- sparse guidance
+ * Replaces marigold_dc.py:706-756 (sparse normalisation), :813-904 (Tweedie preview, learned
+ * affine, l1+l2 loss and its gradient, grad-norm rescale, Adam, DDIM update) and :969-985
+ * (final dense depth).  Per-step scalars are read from device tables indexed by *step so that a
+ * captured hipGraph of one step can be replayed for every timestep.
+ * norm: 0 const, 1 minmax, 2 percentile (host_lohi[2*nb] = quantiles); projection: 0 linear,
+ * 1 log, 2 log10.  params[nb][8] = lo, hi, lo_p, hi_p, min_g, max_g, count, 0.
+ * coef[step][4] = sqrt(a_t), sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev);
+ * adam_tab[step][4] = lr_latent/bc1, sqrt(bc2), lr_affine/bc1, 0.
+ */
+int dc_sparse_setup(const float* sparse, int nb, int h, int w, int norm, float min_depth, float max_depth,
+                    const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt, float* params,
+                    void* stream);
+int dc_preview(const void* x8, const void* v, int nb, int hw, const float* coef, const int* step, void* x0, void* tin,
+               float* eps_norm, void* stream);
+int dc_sparse_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w, const int* idx,
+                   const float* gval, const int* cnt, const float* params, const float* affine, float* dA,
+                   float* daff_grad, float* loss, void* stream);
+int dc_decode_tail_bwd(const void* dec_out, int ldo, const float* dA, int nb, int ph, int pw, int rh, int rw,
+                       void* dout, void* stream);
+int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gunet, int nb, int hw, const float* coef,
+                     const float* adam_tab, const int* step, const float* eps_norm, void* m_lat, void* v_lat,
+                     float* affine, float* m_aff, float* v_aff, const float* daff_grad, float* dbg, void* stream);
+int dc_step_advance(int* step, void* stream);
+int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8, void* stream);
+int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                   const float* params, const float* affine, float* dense, void* stream);
+int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCAMD_H */

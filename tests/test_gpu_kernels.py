@@ -1,0 +1,288 @@
+"""Per-kernel parity of libdcamd.so against plain PyTorch fp32 references of the same op (GPU).
+
+Inputs are rounded to bf16 first, references run in fp32 on the same rounded values; the bar is a
+relative L2 error (bf16 storage of outputs ~ 4e-3) stated per test.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda:0")
+
+
+def rel(a, b):
+    a = a.float()
+    b = b.float()
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from depth_completion_amd.ops import Ctx
+    return Ctx(dev)
+
+
+def nhwc(x):  # NCHW fp32 -> [N*H*W, C] bf16
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c).to(torch.bfloat16).contiguous()
+
+
+def nchw(t, n, h, w):
+    return t.float().reshape(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).float().to(dev)
+
+
+# ----------------------------------------------------------------------------- conv / gemm
+@pytest.mark.parametrize("n,cin,cout,h,w,stride", [
+    (1, 64, 64, 9, 11, 1), (2, 320, 320, 12, 16, 1), (1, 128, 192, 7, 5, 2), (2, 640, 1280, 6, 8, 1),
+    (1, 1280, 1280, 3, 4, 1), (1, 64, 4, 8, 8, 1), (1, 64, 3, 16, 12, 1)])
+def test_conv3x3(ctx, n, cin, cout, h, w, stride):
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    x = rnd(n, cin, h, w, seed=1)
+    wt = rnd(cout, cin, 3, 3, scale=1 / math.sqrt(9 * cin), seed=2)
+    b = rnd(cout, seed=3)
+    ref = F.conv2d(x, wt, b, stride=stride, padding=1)
+    ho, wo = ref.shape[-2:]
+    ldy = max(8, -(-cout // 8) * 8)
+    y = torch.zeros(n * ho * wo, ldy, dtype=torch.bfloat16, device=dev)
+    ops.conv_gemm(ctx, nhwc(x), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=h, win=w, cin=cin, hout=ho, wout=wo,
+                  cout=cout, stride=stride, bias=b, y=y)
+    torch.cuda.synchronize()
+    assert rel(nchw(y[:, :cout], n, ho, wo), ref) < 1e-2
+
+
+def test_conv_epilogues_and_concat(ctx):
+    """two-source input, per-step row bias, residual, relu, relu-backward mask."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    n, c1, c2, cout, h, w = 2, 128, 64, 128, 6, 7
+    xa, xb = rnd(n, c1, h, w, seed=4), rnd(n, c2, h, w, seed=5)
+    wt = rnd(cout, c1 + c2, 3, 3, scale=0.05, seed=6)
+    b = rnd(cout, seed=7)
+    table = rnd(5, cout, seed=8)
+    res = rnd(n, cout, h, w, seed=9)
+    mask = rnd(n, cout, h, w, seed=10)
+    ctx.step.fill_(3)
+    y = torch.empty(n * h * w, cout, dtype=torch.bfloat16, device=dev)
+    ops.conv_gemm(ctx, nhwc(xa), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=h, win=w, cin=c1 + c2, hout=h,
+                  wout=w, cout=cout, x2=nhwc(xb), c1=c1, bias=b, rowbias=table.to(torch.bfloat16), rowbias_ld=cout,
+                  resid=nhwc(res), act=1, mask=nhwc(mask), y=y)
+    torch.cuda.synchronize()
+    ctx.step.zero_()
+    ref = F.conv2d(torch.cat([xa, xb], 1), wt, b, padding=1) + table[3].view(1, -1, 1, 1) + res
+    ref = torch.relu(ref) * (mask > 0)
+    assert rel(nchw(y, n, h, w), ref) < 1e-2
+
+
+def test_conv_upsample_mode(ctx):
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    n, c, h, w = 1, 64, 5, 7
+    for ho, wo in ((10, 14), (9, 13)):
+        x = rnd(n, c, h, w, seed=11)
+        wt = rnd(c, c, 3, 3, scale=0.05, seed=12)
+        ref = F.conv2d(F.interpolate(x, size=(ho, wo), mode="nearest"), wt, padding=1)
+        y = torch.empty(n * ho * wo, c, dtype=torch.bfloat16, device=dev)
+        ops.conv_gemm(ctx, nhwc(x), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=h, win=w, cin=c, hout=ho,
+                      wout=wo, cout=c, mode=1, y=y)
+        torch.cuda.synchronize()
+        assert rel(nchw(y, n, ho, wo), ref) < 1e-2
+
+
+@pytest.mark.parametrize("h,w", [(8, 10), (7, 9)])
+def test_conv_dgrad_modes(ctx, h, w):
+    """input-gradients: stride-1 (flipped weights), stride-2 (mode 2), vs autograd."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv_dgrad
+    n, cin, cout = 2, 64, 128
+    for stride in (1, 2):
+        x = rnd(n, cin, h, w, seed=13).requires_grad_(True)
+        wt = rnd(cout, cin, 3, 3, scale=0.05, seed=14)
+        y = F.conv2d(x, wt, stride=stride, padding=1)
+        gy = rnd(*y.shape, seed=15)
+        y.backward(gy)
+        ho, wo = y.shape[-2:]
+        dx = torch.empty(n * h * w, cin, dtype=torch.bfloat16, device=dev)
+        ops.conv_gemm(ctx, nhwc(gy), pack_conv_dgrad(wt).to(dev, torch.bfloat16), nb=n, hin=ho, win=wo, cin=cout,
+                      hout=h, wout=w, cout=cin, mode=0 if stride == 1 else 2, y=dx)
+        torch.cuda.synchronize()
+        assert rel(nchw(dx, n, h, w), x.grad) < 1e-2, stride
+
+
+def test_small_cin_and_splitk_linear(ctx):
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    # small-C path (cin 8, K padded to 128)
+    n, cin, cout, h, w = 2, 8, 320, 6, 8
+    x = rnd(n, cin, h, w, seed=16)
+    wt = rnd(cout, cin, 3, 3, scale=0.1, seed=17)
+    y = torch.empty(n * h * w, cout, dtype=torch.bfloat16, device=dev)
+    ops.conv_gemm(ctx, nhwc(x), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=h, win=w, cin=cin, hout=h, wout=w,
+                  cout=cout, y=y)
+    torch.cuda.synchronize()
+    assert rel(nchw(y, n, h, w), F.conv2d(x, wt, padding=1)) < 1e-2
+    # linear with deep K and few rows -> split-K path
+    rows, k, m = 100, 5120, 1280
+    a = rnd(rows, k, seed=18)
+    wl = rnd(m, k, scale=1 / math.sqrt(k), seed=19)
+    b = rnd(m, seed=20)
+    res = rnd(rows, m, seed=21)
+    out = torch.empty(rows, m, dtype=torch.bfloat16, device=dev)
+    ops.linear(ctx, a.to(torch.bfloat16), wl.to(torch.bfloat16), rows, m, out, bias=b, resid=res.to(torch.bfloat16))
+    torch.cuda.synchronize()
+    assert rel(out, a @ wl.t() + b + res) < 1e-2
+
+
+# ----------------------------------------------------------------------------- norms
+@pytest.mark.parametrize("c,silu,two", [(320, True, False), (640, False, False), (960, True, True), (64, True, False)])
+def test_groupnorm_fwd_bwd(ctx, c, silu, two):
+    from depth_completion_amd import ops
+    n, h, w = 2, 9, 12
+    x = rnd(n, c, h, w, seed=22) * 2 + 0.5
+    x = x.to(torch.bfloat16).float().requires_grad_(True)
+    gamma = (1 + 0.1 * rnd(c, seed=23)).to(torch.bfloat16).float()
+    beta = (0.1 * rnd(c, seed=24)).to(torch.bfloat16).float()
+    ref = F.group_norm(x, 32, gamma, beta, eps=1e-5)
+    if silu:
+        ref = F.silu(ref)
+    gy = rnd(*ref.shape, seed=25)
+    ref.backward(gy)
+    xs = nhwc(x.detach())
+    y = torch.empty_like(xs)
+    stats = torch.empty(n, 32, 2, device=dev)
+    c1 = 640 if two else 0
+    if two:
+        xa, xb = xs[:, :c1].contiguous(), xs[:, c1:].contiguous()
+        ops.groupnorm(ctx, xa, n, h * w, c, gamma, beta, 1e-5, silu, y, stats, x2=xb, c1=c1)
+    else:
+        ops.groupnorm(ctx, xs, n, h * w, c, gamma, beta, 1e-5, silu, y, stats)
+    dx = torch.empty_like(xs)
+    add = nhwc(gy)
+    if two:
+        ops.groupnorm_bwd(ctx, xa, n, h * w, c, gamma, beta, silu, stats, nhwc(gy), dx, x2=xb, c1=c1, add1=add)
+    else:
+        ops.groupnorm_bwd(ctx, xs, n, h * w, c, gamma, beta, silu, stats, nhwc(gy), dx, add1=add)
+    torch.cuda.synchronize()
+    assert rel(nchw(y, n, h, w), ref) < 1e-2
+    assert rel(nchw(dx, n, h, w), x.grad + gy) < 2e-2
+
+
+@pytest.mark.parametrize("c", [64, 320, 1280])
+def test_layernorm_fwd_bwd(ctx, c):
+    from depth_completion_amd import ops
+    rows = 333
+    x = (rnd(rows, c, seed=26) * 3 + 1).to(torch.bfloat16).float().requires_grad_(True)
+    gamma = (1 + 0.1 * rnd(c, seed=27)).to(torch.bfloat16).float()
+    beta = (0.1 * rnd(c, seed=28)).to(torch.bfloat16).float()
+    ref = F.layer_norm(x, (c,), gamma, beta, 1e-5)
+    gy = rnd(rows, c, seed=29)
+    ref.backward(gy)
+    y = torch.empty(rows, c, dtype=torch.bfloat16, device=dev)
+    st = torch.empty(rows, 2, device=dev)
+    ops.layernorm(ctx, x.detach().to(torch.bfloat16), rows, c, gamma, beta, 1e-5, y, st)
+    dx = torch.empty_like(y)
+    ops.layernorm_bwd(ctx, x.detach().to(torch.bfloat16), rows, c, gamma, st, gy.to(torch.bfloat16), dx)
+    torch.cuda.synchronize()
+    assert rel(y, ref) < 1e-2
+    assert rel(dx, x.grad) < 2e-2
+
+
+# ----------------------------------------------------------------------------- attention
+@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (2, 300, 2), (1, 1000, 5), (1, 108, 20)])
+def test_attention_fwd_bwd(ctx, n, t, heads):
+    from depth_completion_amd import ops
+    C = heads * 64
+    qkv = rnd(n, t, 3 * C, seed=30).to(torch.bfloat16).float().requires_grad_(True)
+    q, k, v = qkv.split(C, -1)
+    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
+    o = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
+    do = rnd(n, t, C, seed=31)
+    o.backward(do)
+    qkv_b = qkv.detach().to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
+    ob = torch.empty(n * t, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(n, heads, t, device=dev)
+    ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
+    dq = torch.empty_like(qkv_b)
+    delta = torch.empty(n, heads, t, device=dev)
+    ops.attn_bwd(ctx, qkv_b, ob, do.to(torch.bfloat16).reshape(n * t, C), lse, n, t, heads, delta, dq)
+    torch.cuda.synchronize()
+    assert rel(ob.view(n, t, C), o) < 1e-2
+    s = torch.einsum("nhqd,nhkd->nhqk", sh(q).detach(), sh(k).detach()) / 8
+    assert rel(lse, torch.logsumexp(s, -1)) < 1e-4
+    assert rel(dq.view(n, t, 3 * C), qkv.grad) < 2e-2
+
+
+def test_cross_attention_fold(ctx):
+    """Folded 2-key cross-attention == LN2 + attn2 (2-token context) + residual."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import fold_cross_attention
+    rows, C, heads, cross = 257, 320, 5, 1024
+    g = torch.Generator().manual_seed(32)
+    sd = {"to_q.weight": torch.randn(C, C, generator=g) / math.sqrt(C),
+          "to_k.weight": torch.randn(C, cross, generator=g) / math.sqrt(cross),
+          "to_v.weight": torch.randn(C, cross, generator=g) / math.sqrt(cross),
+          "to_out.0.weight": torch.randn(C, C, generator=g) / math.sqrt(C),
+          "to_out.0.bias": torch.randn(C, generator=g) * 0.1}
+    ctxt = torch.randn(2, cross, generator=g)
+    U, D, c0 = [t.to(dev) for t in fold_cross_attention(sd, "", ctxt, heads)]
+    gamma = (1 + 0.1 * torch.randn(C, generator=g)).to(torch.bfloat16).float().to(dev)
+    beta = (0.1 * torch.randn(C, generator=g)).to(torch.bfloat16).float().to(dev)
+    x = (torch.randn(rows, C, generator=g) * 2).to(torch.bfloat16).float().to(dev).requires_grad_(True)
+    bf = lambda t: t.to(torch.bfloat16).float().to(dev)  # noqa: E731
+    nrm = F.layer_norm(x, (C,), gamma, beta, 1e-5)
+    q = nrm @ bf(sd["to_q.weight"]).t()
+    k = bf(ctxt) @ bf(sd["to_k.weight"]).t()
+    v = bf(ctxt) @ bf(sd["to_v.weight"]).t()
+    sh = lambda z: z.view(-1, heads, 64).transpose(0, 1)  # noqa: E731
+    att = torch.softmax(sh(q) @ sh(k).transpose(1, 2) / 8, -1) @ sh(v)
+    out = att.transpose(0, 1).reshape(rows, C) @ bf(sd["to_out.0.weight"]).t() + bf(sd["to_out.0.bias"]) + x
+    dy = rnd(rows, C, seed=33)
+    out.backward(dy)
+    y = torch.empty(rows, C, dtype=torch.bfloat16, device=dev)
+    st = torch.empty(rows, 2, device=dev)
+    pr = torch.empty(rows, heads, device=dev)
+    xb = x.detach().to(torch.bfloat16)
+    ops.crossattn_fwd(ctx, xb, rows, C, heads, 1e-5, gamma, beta, U, D, c0, y, st, pr)
+    dx = torch.empty_like(y)
+    ops.crossattn_bwd(ctx, xb, rows, C, heads, gamma, U, D, st, pr, dy.to(torch.bfloat16), dx)
+    torch.cuda.synchronize()
+    assert rel(y, out) < 1e-2
+    assert rel(dx, x.grad) < 2e-2
+
+
+# ----------------------------------------------------------------------------- elementwise
+def test_geglu_and_upsample_adjoint(ctx):
+    from depth_completion_amd import ops
+    rows, c = 123, 256
+    f = rnd(rows, 2 * c, seed=34).requires_grad_(True)
+    hh, gg = f.chunk(2, -1)
+    y = hh * F.gelu(gg)
+    dy = rnd(rows, c, seed=35)
+    y.backward(dy)
+    yb = torch.empty(rows, c, dtype=torch.bfloat16, device=dev)
+    ops.geglu(ctx, f.detach().to(torch.bfloat16), rows, c, yb)
+    df = torch.empty(rows, 2 * c, dtype=torch.bfloat16, device=dev)
+    ops.geglu_bwd(ctx, f.detach().to(torch.bfloat16), rows, c, dy.to(torch.bfloat16), df)
+    torch.cuda.synchronize()
+    assert rel(yb, y) < 1e-2 and rel(df, f.grad) < 2e-2
+    # nearest-upsample adjoint (x2 and a non-integer size)
+    for (hl, wl), (hh_, wh) in (((5, 7), (10, 14)), ((7, 12), (14, 24)), ((4, 12), (7, 24))):
+        x = rnd(2, 64, hl, wl, seed=36).requires_grad_(True)
+        up = F.interpolate(x, size=(hh_, wh), mode="nearest")
+        g = rnd(*up.shape, seed=37)
+        up.backward(g)
+        out = torch.empty(2 * hl * wl, 64, dtype=torch.bfloat16, device=dev)
+        ops.upsample_adjoint(ctx, nhwc(g), 2, hh_, wh, 64, hl, wl, out)
+        torch.cuda.synchronize()
+        assert rel(nchw(out, 2, hl, wl), x.grad) < 1e-2
