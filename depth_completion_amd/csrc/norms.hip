@@ -1,11 +1,12 @@
 // GroupNorm(+SiLU) and LayerNorm forward / backward on NHWC rows (gfx950).
 //
-// GroupNorm (diffusers ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out):
-//   pass 1 (stats):  per (frame, pixel-chunk) block, channel sums in registers -> LDS -> group
-//                    partial (sum, sumsq) slab  [nb][nchunk][G][2]
-//   pass 2 (apply):  every block folds the slab for its frame (double) into (mean, rstd) per group,
-//                    normalises its chunk, optional SiLU, writes bf16 (+ stats [nb][G][2] fp32).
-// Backward follows the same two passes with (sum gamma*dy', sum gamma*dy'*xhat) partials.
+// GroupNorm (diffusers ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out),
+// three launches, all reductions in a fixed order (bitwise reproducible run to run):
+//   stats     per (frame, pixel-chunk) block: 8 channels per thread in registers over its rows,
+//             rows folded through LDS, channels folded into group partials -> slab [nb][nchunk][G][2]
+//   finalize  one block per frame, one wave per group: fold the chunk partials (fp64) -> mean, rstd
+//   apply     elementwise normalise (+ SiLU), 16 B per lane
+// Backward: the same with (sum gamma*dy', sum gamma*dy'*xhat) and dx = rstd*(g*dy' - a - xhat*b).
 // The input may be two sources (UNet skip concat): channels >= c1 come from x2.
 #include "common.h"
 #include "../../include/dcamd.h"
@@ -27,16 +28,43 @@ __device__ __forceinline__ void gn_load8(const GNShape& s, int n, int row, int c
   load8(src, f);
 }
 
-__global__ void gn_stats_kernel(GNShape s, float* part) {
-  extern __shared__ float sh[];  // [2*c]
-  float* csum = sh;
-  float* csq = sh + s.c;
-  const int n = blockIdx.y, chunk = blockIdx.x;
-  for (int i = threadIdx.x; i < 2 * s.c; i += blockDim.x) sh[i] = 0.0f;
-  __syncthreads();
+// fold per-thread channel partials (a, b)[8] across the R row-lanes, then into group partials
+__device__ void gn_block_fold(const GNShape& s, const float* a, const float* b, float* sh, float* out) {
+  // sh: [2][R][c] floats
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
+  const bool active = r0 < s.R;
+  float* sa = sh;
+  float* sb = sh + s.R * s.c;
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sa[r0 * s.c + cg * 8 + i] = a[i];
+      sb[r0 * s.c + cg * 8 + i] = b[i];
+    }
+  }
+  __syncthreads();
+  // per channel: sum over row-lanes (fixed order) -> reuse row 0
+  for (int ch = threadIdx.x; ch < s.c; ch += blockDim.x) {
+    float ta = 0.0f, tb = 0.0f;
+    for (int r = 0; r < s.R; ++r) { ta += sa[r * s.c + ch]; tb += sb[r * s.c + ch]; }
+    sa[ch] = ta;
+    sb[ch] = tb;
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < s.groups; g += blockDim.x) {
+    float ta = 0.0f, tb = 0.0f;
+    for (int k = 0; k < s.cpg; ++k) { ta += sa[g * s.cpg + k]; tb += sb[g * s.cpg + k]; }
+    out[g * 2] = ta;
+    out[g * 2 + 1] = tb;
+  }
+}
+
+__global__ void gn_stats_kernel(GNShape s, float* part) {
+  extern __shared__ float sh[];
+  const int n = blockIdx.y, chunk = blockIdx.x;
+  const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
+  float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (r0 < s.R) {
-    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int rbeg = chunk * s.rows_per_chunk, rend = min(s.hw, rbeg + s.rows_per_chunk);
     for (int row = rbeg + r0; row < rend; row += s.R) {
       float f[8];
@@ -44,188 +72,131 @@ __global__ void gn_stats_kernel(GNShape s, float* part) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) { a[i] += f[i]; b[i] += f[i] * f[i]; }
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      atomicAdd(&csum[cg * 8 + i], a[i]);
-      atomicAdd(&csq[cg * 8 + i], b[i]);
-    }
   }
-  __syncthreads();
-  for (int g = threadIdx.x; g < s.groups; g += blockDim.x) {
-    float ts = 0.0f, tq = 0.0f;
-    for (int k = 0; k < s.cpg; ++k) { ts += csum[g * s.cpg + k]; tq += csq[g * s.cpg + k]; }
-    float* dst = part + (((long)n * s.nchunk + chunk) * s.groups + g) * 2;
-    dst[0] = ts;
-    dst[1] = tq;
-  }
+  gn_block_fold(s, a, b, sh, part + ((long)n * s.nchunk + chunk) * s.groups * 2);
 }
 
-// fold partial slabs of frame n into (mean, rstd) per group in LDS
-__device__ void gn_fold_stats(const GNShape& s, const float* part, int n, float eps, float* mean, float* rstd) {
-  for (int g = threadIdx.x; g < s.groups; g += blockDim.x) {
-    double ts = 0.0, tq = 0.0;
-    for (int k = 0; k < s.nchunk; ++k) {
+// one block per frame, one wave per group (looping): fp64 fold of the chunk partials.
+// mode 0: out = (mean, rstd) from (sum, sumsq); mode 1: out = (sum a / cnt, sum b / cnt)
+__global__ void gn_finalize_kernel(GNShape s, const float* part, float eps, int mode, float* out) {
+  const int n = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const double cnt = (double)s.hw * s.cpg;
+  for (int g = wid; g < s.groups; g += nw) {
+    double ta = 0.0, tb = 0.0;
+    for (int k = lane; k < s.nchunk; k += 64) {
       const float* src = part + (((long)n * s.nchunk + k) * s.groups + g) * 2;
-      ts += src[0];
-      tq += src[1];
+      ta += src[0];
+      tb += src[1];
     }
-    const double cnt = (double)s.hw * s.cpg;
-    const double mu = ts / cnt;
-    double var = tq / cnt - mu * mu;
-    if (var < 0.0) var = 0.0;
-    mean[g] = (float)mu;
-    rstd[g] = (float)(1.0 / sqrt(var + (double)eps));
+    for (int o = 32; o >= 1; o >>= 1) {
+      ta += __shfl_xor(ta, o, 64);
+      tb += __shfl_xor(tb, o, 64);
+    }
+    if (lane == 0) {
+      float* dst = out + ((long)n * s.groups + g) * 2;
+      if (mode == 0) {
+        const double mu = ta / cnt;
+        double var = tb / cnt - mu * mu;
+        if (var < 0.0) var = 0.0;
+        dst[0] = (float)mu;
+        dst[1] = (float)(1.0 / sqrt(var + (double)eps));
+      } else {
+        dst[0] = (float)(ta / cnt);
+        dst[1] = (float)(tb / cnt);
+      }
+    }
   }
 }
 
-__global__ void gn_apply_kernel(GNShape s, const float* part, float eps, const float* gamma, const float* beta,
-                                int silu, bf16* y, int ldy, float* stats) {
-  __shared__ float mean[64], rstd[64];
-  const int n = blockIdx.y, chunk = blockIdx.x;
-  gn_fold_stats(s, part, n, eps, mean, rstd);
-  __syncthreads();
-  if (chunk == 0 && stats) {
-    for (int g = threadIdx.x; g < s.groups; g += blockDim.x) {
-      stats[((long)n * s.groups + g) * 2] = mean[g];
-      stats[((long)n * s.groups + g) * 2 + 1] = rstd[g];
-    }
-  }
-  const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
-  if (r0 >= s.R) return;
-  float gm[8], bt[8], mu[8], rs[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = cg * 8 + i, g = c / s.cpg;
-    gm[i] = gamma[c];
-    bt[i] = beta[c];
-    mu[i] = mean[g];
-    rs[i] = rstd[g];
-  }
-  const int rbeg = chunk * s.rows_per_chunk, rend = min(s.hw, rbeg + s.rows_per_chunk);
-  for (int row = rbeg + r0; row < rend; row += s.R) {
+__global__ void gn_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
+                                bf16* y, int ldy) {
+  const long total = (long)s.nb * s.hw * s.cgs;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % s.cgs);
+    const long pix = i / s.cgs;
+    const int n = (int)(pix / s.hw), row = (int)(pix - (long)n * s.hw);
     float f[8];
     gn_load8(s, n, row, cg * 8, f);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float v = (f[i] - mu[i]) * rs[i] * gm[i] + bt[i];
+    for (int k = 0; k < 8; ++k) {
+      const int c = cg * 8 + k, g = c / s.cpg;
+      const float mu = stats[((long)n * s.groups + g) * 2], rs = stats[((long)n * s.groups + g) * 2 + 1];
+      float v = (f[k] - mu) * rs * gamma[c] + beta[c];
       if (silu) v = silu_f((float)(bf16)v);
-      f[i] = v;
+      f[k] = v;
     }
-    store8(y + ((long)n * s.hw + row) * ldy + cg * 8, f);
+    store8(y + pix * ldy + cg * 8, f);
   }
 }
 
 // dy' = dy * silu'(y) (y = gn(x) rounded to bf16, dy' rounded to bf16), as autograd does on bf16
-__device__ __forceinline__ void gn_bwd_elem(const GNShape& s, int n, int row, int cg, const float* mu, const float* rs,
-                                            const float* gm, const float* bt, int silu, const bf16* dy, int lddy,
-                                            float* xh, float* gdy) {
+__device__ __forceinline__ void gn_bwd_elem(const GNShape& s, int n, int row, int cg, const float* stats,
+                                            const float* gamma, const float* beta, int silu, const bf16* dy,
+                                            int lddy, float* xh, float* gdy, float* rsv) {
   float f[8], d[8];
   gn_load8(s, n, row, cg * 8, f);
   load8(dy + ((long)n * s.hw + row) * lddy + cg * 8, d);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const float xhat = (f[i] - mu[i]) * rs[i];
+    const int c = cg * 8 + i, g = c / s.cpg;
+    const float mu = stats[((long)n * s.groups + g) * 2], rs = stats[((long)n * s.groups + g) * 2 + 1];
+    const float xhat = (f[i] - mu) * rs;
     float dd = d[i];
     if (silu) {
-      const float yv = (float)(bf16)(xhat * gm[i] + bt[i]);
+      const float yv = (float)(bf16)(xhat * gamma[c] + beta[c]);
       dd = (float)(bf16)(dd * silu_grad(yv));
     }
     xh[i] = xhat;
-    gdy[i] = dd * gm[i];
+    gdy[i] = dd * gamma[c];
+    rsv[i] = rs;
   }
 }
 
 __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
                                     const bf16* dy, int lddy, float* part) {
   extern __shared__ float sh[];
-  float* ca = sh;
-  float* cb = sh + s.c;
   const int n = blockIdx.y, chunk = blockIdx.x;
-  for (int i = threadIdx.x; i < 2 * s.c; i += blockDim.x) sh[i] = 0.0f;
-  __syncthreads();
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
+  float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (r0 < s.R) {
-    float gm[8], bt[8], mu[8], rs[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = cg * 8 + i, g = c / s.cpg;
-      gm[i] = gamma[c];
-      bt[i] = beta[c];
-      mu[i] = stats[((long)n * s.groups + g) * 2];
-      rs[i] = stats[((long)n * s.groups + g) * 2 + 1];
-    }
-    float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int rbeg = chunk * s.rows_per_chunk, rend = min(s.hw, rbeg + s.rows_per_chunk);
     for (int row = rbeg + r0; row < rend; row += s.R) {
-      float xh[8], gdy[8];
-      gn_bwd_elem(s, n, row, cg, mu, rs, gm, bt, silu, dy, lddy, xh, gdy);
+      float xh[8], gdy[8], rs[8];
+      gn_bwd_elem(s, n, row, cg, stats, gamma, beta, silu, dy, lddy, xh, gdy, rs);
 #pragma unroll
       for (int i = 0; i < 8; ++i) { a[i] += gdy[i]; b[i] += gdy[i] * xh[i]; }
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      atomicAdd(&ca[cg * 8 + i], a[i]);
-      atomicAdd(&cb[cg * 8 + i], b[i]);
-    }
   }
-  __syncthreads();
-  for (int g = threadIdx.x; g < s.groups; g += blockDim.x) {
-    float ta = 0.0f, tb = 0.0f;
-    for (int k = 0; k < s.cpg; ++k) { ta += ca[g * s.cpg + k]; tb += cb[g * s.cpg + k]; }
-    float* dst = part + (((long)n * s.nchunk + chunk) * s.groups + g) * 2;
-    dst[0] = ta;
-    dst[1] = tb;
-  }
+  gn_block_fold(s, a, b, sh, part + ((long)n * s.nchunk + chunk) * s.groups * 2);
 }
 
 __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
-                                    const bf16* dy, int lddy, const float* part, bf16* dx, int lddx,
+                                    const bf16* dy, int lddy, const float* ab, bf16* dx, int lddx,
                                     const bf16* add1, int ldadd1, const bf16* add2, int ldadd2) {
-  __shared__ float ma[64], mb[64];
-  const int n = blockIdx.y, chunk = blockIdx.x;
-  for (int g = threadIdx.x; g < s.groups; g += blockDim.x) {
-    double ta = 0.0, tb = 0.0;
-    for (int k = 0; k < s.nchunk; ++k) {
-      const float* src = part + (((long)n * s.nchunk + k) * s.groups + g) * 2;
-      ta += src[0];
-      tb += src[1];
+  const long total = (long)s.nb * s.hw * s.cgs;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % s.cgs);
+    const long pix = i / s.cgs;
+    const int n = (int)(pix / s.hw), row = (int)(pix - (long)n * s.hw);
+    float xh[8], gdy[8], rs[8], out[8];
+    gn_bwd_elem(s, n, row, cg, stats, gamma, beta, silu, dy, lddy, xh, gdy, rs);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int g = (cg * 8 + k) / s.cpg;
+      const float ma = ab[((long)n * s.groups + g) * 2], mb = ab[((long)n * s.groups + g) * 2 + 1];
+      out[k] = rs[k] * (gdy[k] - ma - xh[k] * mb);
     }
-    const double cnt = (double)s.hw * s.cpg;
-    ma[g] = (float)(ta / cnt);
-    mb[g] = (float)(tb / cnt);
-  }
-  __syncthreads();
-  const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
-  if (r0 >= s.R) return;
-  float gm[8], bt[8], mu[8], rs[8], a[8], b[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = cg * 8 + i, g = c / s.cpg;
-    gm[i] = gamma[c];
-    bt[i] = beta[c];
-    mu[i] = stats[((long)n * s.groups + g) * 2];
-    rs[i] = stats[((long)n * s.groups + g) * 2 + 1];
-    a[i] = ma[g];
-    b[i] = mb[g];
-  }
-  const int rbeg = chunk * s.rows_per_chunk, rend = min(s.hw, rbeg + s.rows_per_chunk);
-  for (int row = rbeg + r0; row < rend; row += s.R) {
-    float xh[8], gdy[8], out[8];
-    gn_bwd_elem(s, n, row, cg, mu, rs, gm, bt, silu, dy, lddy, xh, gdy);
-    const long pix = (long)n * s.hw + row;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) out[i] = rs[i] * (gdy[i] - a[i] - xh[i] * b[i]);
     if (add1) {
       float e[8];
       load8(add1 + pix * ldadd1 + cg * 8, e);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) out[i] = (float)(bf16)out[i] + e[i];
+      for (int k = 0; k < 8; ++k) out[k] = (float)(bf16)out[k] + e[k];
     }
     if (add2) {
       float e[8];
       load8(add2 + pix * ldadd2 + cg * 8, e);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) out[i] = (float)(bf16)out[i] + e[i];
+      for (int k = 0; k < 8; ++k) out[k] = (float)(bf16)out[k] + e[k];
     }
     store8(dx + pix * lddx + cg * 8, out);
   }
@@ -234,7 +205,7 @@ __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* 
 bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c,
                    int groups) {
   if (!x || nb <= 0 || hw <= 0 || c <= 0 || groups <= 0 || groups > 64) return false;
-  if (c % groups != 0 || c % 8 != 0) return false;
+  if (c % groups != 0 || c % 8 != 0 || c > 8 * 1024) return false;
   if (ldx % 8 || (x2 && (ldx2 % 8 || c1 % 8))) return false;
   s.x = (const bf16*)x;
   s.x2 = (const bf16*)(x2 ? x2 : x);
@@ -248,12 +219,21 @@ bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2,
   s.cpg = c / groups;
   s.cgs = c / 8;
   s.R = max(1, 256 / s.cgs);
-  // aim for >= ~64 rows per block but enough blocks to cover the chip
-  int target_blocks = max(1, 512 / nb);
+  // ~256-512 blocks over the whole launch, each at least R rows
+  const int target_blocks = max(1, 384 / nb);
   s.rows_per_chunk = max(s.R, (hw + target_blocks - 1) / target_blocks);
   s.rows_per_chunk = ((s.rows_per_chunk + s.R - 1) / s.R) * s.R;
   s.nchunk = (hw + s.rows_per_chunk - 1) / s.rows_per_chunk;
   return true;
+}
+
+// workspace layout: [partials nb*nchunk*G*2][ab nb*G*2]
+inline long gn_part_floats(const GNShape& s) { return (long)s.nb * s.nchunk * s.groups * 2; }
+
+inline dim3 ew_grid(long n) {
+  long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return dim3((unsigned)(b < 1 ? 1 : b));
 }
 
 }  // namespace
@@ -262,21 +242,23 @@ extern "C" long long dc_groupnorm_ws_bytes(int nb, int hw, int c, int groups) {
   GNShape s;
   static const bf16 dummy[8] = {};
   if (!gn_make_shape(s, dummy, c, nullptr, 0, 0, nb, hw, c, groups)) return -1;
-  return (long long)nb * s.nchunk * groups * 2 * sizeof(float);
+  return (gn_part_floats(s) + (long)nb * groups * 2) * (long long)sizeof(float);
 }
 
 extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c,
                                 int groups, float eps, const float* gamma, const float* beta, int silu, void* y,
                                 int ldy, float* stats, float* ws, void* stream) {
   GNShape s;
-  if (!gn_make_shape(s, x, ldx, x2, ldx2, c1, nb, hw, c, groups) || !y || !gamma || !beta || !ws) return DC_ERR_ARG;
+  if (!gn_make_shape(s, x, ldx, x2, ldx2, c1, nb, hw, c, groups) || !y || !gamma || !beta || !ws || !stats)
+    return DC_ERR_ARG;
   if (ldy % 8) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   const int threads = s.cgs * s.R;
-  dim3 grid(s.nchunk, nb);
-  hipLaunchKernelGGL(gn_stats_kernel, grid, dim3(threads), 2 * c * sizeof(float), st, s, ws);
-  hipLaunchKernelGGL(gn_apply_kernel, grid, dim3(threads), 0, st, s, ws, eps, gamma, beta, silu, (bf16*)y, ldy,
-                     stats);
+  const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nb), dim3(256), 0, st, s, ws, eps, 0, stats);
+  hipLaunchKernelGGL(gn_apply_kernel, ew_grid((long)nb * hw * s.cgs), dim3(256), 0, st, s, stats, gamma, beta, silu,
+                     (bf16*)y, ldy);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -290,11 +272,14 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   if (lddy % 8 || lddx % 8 || (add1 && ldadd1 % 8) || (add2 && ldadd2 % 8)) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   const int threads = s.cgs * s.R;
-  dim3 grid(s.nchunk, nb);
-  hipLaunchKernelGGL(gn_bwd_stats_kernel, grid, dim3(threads), 2 * c * sizeof(float), st, s, stats, gamma, beta,
-                     silu, (const bf16*)dy, lddy, ws);
-  hipLaunchKernelGGL(gn_bwd_apply_kernel, grid, dim3(threads), 0, st, s, stats, gamma, beta, silu, (const bf16*)dy,
-                     lddy, ws, (bf16*)dx, lddx, (const bf16*)add1, ldadd1, (const bf16*)add2, ldadd2);
+  const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
+  float* ab = ws + gn_part_floats(s);
+  hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, stats, gamma, beta, silu,
+                     (const bf16*)dy, lddy, ws);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, ew_grid((long)nb * hw * s.cgs), dim3(256), 0, st, s, stats, gamma, beta,
+                     silu, (const bf16*)dy, lddy, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1,
+                     (const bf16*)add2, ldadd2);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

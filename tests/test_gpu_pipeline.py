@@ -2,10 +2,12 @@
 
 The oracle (oracle/pipeline_ref.py, pinned bit-exactly to the reference's own loop code by
 tests/test_oracle_golden.py) runs the same synthetic weights, inputs and initial noise.  Parity
-statement: after fitting each dense output to the sparse points with the reference's
-closed-form affine (compute_affine_params, marigold_dc.py:53-128), the per-pixel |depth difference|
-has mean <= 0.5 % and p99 <= 2 % of the frame's depth range (bf16 end-to-end), and the HIP result is
-no further from the fp32 oracle than the oracle's own bf16 execution is (x2 margin).
+statement (tolerances set from measurement): after fitting each dense output to the
+sparse points with the reference's closed-form affine (compute_affine_params, marigold_dc.py:53-128),
+the per-pixel |depth difference| to the fp32 oracle, relative to the frame's depth range, is at most
+2x the oracle's own bf16 execution's (+1e-3), and below mean 2 % / p99 8 % absolute.  With synthetic
+weights the bf16 oracle itself sits at ~1.1 % mean / 4.5 % p99 after 10 guided steps, so the survey's
+proposed 0.5 % / 2 % is below the bf16 noise floor of the reference path itself.
 """
 import pytest
 import torch
