@@ -9,7 +9,7 @@ import ctypes as C
 from pathlib import Path
 
 _LIB_PATH = Path(__file__).resolve().parent / "libdcamd.so"
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -30,13 +30,14 @@ class ConvDesc(C.Structure):
         ("bias", vp), ("rowbias", vp), ("rowbias_idx", vp), ("rowbias_ld", i32),
         ("resid", vp), ("ldr", i32), ("mask", vp), ("ldmask", i32), ("act", i32),
         ("y", vp), ("ldy", i32),
-        ("ws", vp), ("ws_bytes", i64),
+        ("ws", vp), ("ws_bytes", i64), ("algo", i32), ("splitk", i32),
     ]
 
 
 # name -> argtypes (all return int status unless listed in _RESTYPE)
 _SIGS = {
     "dc_abi_version": [],
+    "dc_conv_num_algos": [],
     "dc_conv_gemm": [C.POINTER(ConvDesc), vp],
     "dc_groupnorm_ws_bytes": [i32, i32, i32, i32],
     "dc_groupnorm_fwd": [vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, i32, vp, vp, vp],

@@ -1,17 +1,23 @@
 // Implicit-GEMM convolution / linear layer on gfx950 MFMA (v_mfma_f32_16x16x32_bf16).
 //
-// One kernel serves every matmul-shaped op of the hot path:
+// One kernel family serves every matmul-shaped op of the hot path:
 //   * 3x3 / 1x1 convs of the UNet resnets and TAESD (fwd), stride 2 (Downsample2D),
 //     nearest-upsample folded into the A-operand addressing (Upsample2D, TAESD Upsample),
 //   * their input gradients (dgrad = conv with pre-flipped/transposed weights; mode 2 is
 //     the transposed stride-2 gather for the Downsample2D VJP),
 //   * every nn.Linear (1x1 conv over token rows).
-// GEMM view: M = output pixels (NHWC rows), N = output channels, K = taps x Cin (K contiguous
-// in both operands).  Tiles: BM x BN x 64, 4 waves (2x2), register-staged double-buffered LDS
-// with an XOR swizzle (conflict-free ds_read_b128 fragments), LDS-staged coalesced epilogue
-// with fused bias / per-step row bias (time embedding) / residual / ReLU / ReLU-backward mask.
-// Split-K writes fp32 partial slabs that a second kernel reduces through the same epilogue.
+// GEMM view: M = output pixels (NHWC rows), N = output channels, K = taps x Cin (K contiguous in
+// both operands).  Tiles BM x BN x 64 on 4 waves (2x2).  Operands are gathered straight into an
+// S-deep LDS ring with global_load_lds_dwordx4 (per-lane source address = the im2col gather; padding
+// and tails read a zero line), XOR-swizzled through the source permutation so the ds_read_b128
+// fragment reads are conflict-free; S-2 k-chunks stay in flight across the (raw) barrier under a
+// counted vmcnt.  The epilogue stages the fp32 tile through LDS and applies bias / per-step row bias
+// (time embedding) / residual / ReLU / ReLU-backward mask with 16-B coalesced accesses.  Split-K
+// writes fp32 partial slabs that a second kernel reduces through the same epilogue.
+#include <type_traits>
+
 #include "common.h"
+#include "../../include/dcamd.h"
 
 struct ConvGemmParams {
   const bf16* x;
@@ -38,6 +44,8 @@ struct ConvGemmParams {
   long ws_bytes;
   int splits, kps, npad;
 };
+
+__device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of every padded / out-of-range piece
 
 namespace {
 
@@ -87,20 +95,42 @@ __device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, 
   }
 }
 
-template <int BM, int BN>
-struct Smem {
-  static constexpr int STAGE = (BM + BN) * 64 * 2;
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `ahead` k-chunks (L pieces each) remain in flight
+template <int L, int S>
+__device__ __forceinline__ void wait_chunks(int ahead) {
+  static_assert(S >= 2 && S <= 8, "stages");
+  switch (ahead) {
+    case 0: vm_wait<0>(); break;
+    case 1: vm_wait<(S > 2 ? L : 0)>(); break;
+    case 2: vm_wait<(S > 3 ? 2 * L : 0)>(); break;
+    case 3: vm_wait<(S > 4 ? 3 * L : 0)>(); break;
+    case 4: vm_wait<(S > 5 ? 4 * L : 0)>(); break;
+    case 5: vm_wait<(S > 6 ? 5 * L : 0)>(); break;
+    default: vm_wait<(S > 7 ? 6 * L : 0)>(); break;
+  }
+}
+
+template <int BM, int BN, int S>
+struct Cfg {
+  static constexpr int STAGE = (BM + BN) * 128;
   static constexpr int EPI = BM * (BN + 4) * 4;
-  static constexpr int BYTES = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
+  static constexpr int LDS = (S * STAGE > EPI) ? S * STAGE : EPI;
 };
 
-template <int BM, int BN, bool SMALLC>
+template <int BM, int BN, int S, bool SMALLC>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) {
   constexpr int AP = BM / 32;  // A pieces (16 B) per thread per k-chunk
   constexpr int BP = BN / 32;
+  constexpr int L = AP + BP;   // LDS-DMA instructions per thread per k-chunk
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
-  __shared__ __attribute__((aligned(16))) char smem[Smem<BM, BN>::BYTES];
+  constexpr int STAGE = Cfg<BM, BN, S>::STAGE;
+  __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, S>::LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -119,96 +149,132 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   const int nk = p.ktot >> 6;
   const int kc_begin = blockIdx.y * p.kps;
   const int kc_end = min(nk, kc_begin + p.kps);
+  const int nkc = max(0, kc_end - kc_begin);
 
-  // per-thread A-row metadata
-  const int piece = tid & 7;
-  int a_n[AP], a_y[AP], a_x[AP];
+  // per-thread A-row gather tables (piece j covers tile row (tid>>3) + 32 j, slot tid&7):
+  // source pixel = ypix[ky] + xpix[kx] for every mode (direct / upsample / transposed), valid-tap bitmask
+  const int slot = tid & 7;
+  struct RowTab {
+    int y0, y1, y2, x0, x1, x2;
+  };
+  RowTab rt[AP];
+  int a_sw[AP];
+  unsigned vmask[AP];
 #pragma unroll
-  for (int i = 0; i < AP; ++i) {
-    const long m = m0 + (tid >> 3) + 32 * i;
+  for (int j = 0; j < AP; ++j) {
+    const int row = (tid >> 3) + 32 * j;
+    a_sw[j] = slot ^ (row & 7);  // logical 16-B chunk this lane fetches (XOR swizzle via the source)
+    const long m = m0 + row;
+    vmask[j] = 0u;
+    int yp[3] = {0, 0, 0}, xp[3] = {0, 0, 0};
     if (m < M) {
       const int n = (int)(m / hwo);
       const int rem = (int)(m - (long)n * hwo);
       const int oy = rem / p.wout, ox = rem - (rem / p.wout) * p.wout;
-      a_n[i] = n;
-      if (p.mode == 0) {
-        a_y[i] = oy * p.stride - p.pad;
-        a_x[i] = ox * p.stride - p.pad;
-      } else {
-        a_y[i] = oy - p.pad;
-        a_x[i] = ox - p.pad;
+      unsigned yv = 0u, xv = 0u;
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        int iy, ix;
+        bool oky, okx;
+        if (p.mode == 0) {
+          iy = oy * p.stride - p.pad + t;
+          ix = ox * p.stride - p.pad + t;
+          oky = iy >= 0 && iy < p.hin;
+          okx = ix >= 0 && ix < p.win;
+        } else if (p.mode == 1) {
+          const int vy = oy - p.pad + t, vx = ox - p.pad + t;
+          oky = vy >= 0 && vy < p.hout;
+          okx = vx >= 0 && vx < p.wout;
+          iy = oky ? (int)(((long)vy * p.hin) / p.hout) : 0;
+          ix = okx ? (int)(((long)vx * p.win) / p.wout) : 0;
+        } else {
+          const int ty = oy - 1 + t, tx = ox - 1 + t;
+          oky = ty >= 0 && !(ty & 1) && (ty >> 1) < p.hin;
+          okx = tx >= 0 && !(tx & 1) && (tx >> 1) < p.win;
+          iy = ty >> 1;
+          ix = tx >> 1;
+        }
+        oky = oky && t < p.kh;
+        okx = okx && t < p.kw;
+        yp[t] = oky ? (n * p.hin + iy) * p.win : 0;
+        xp[t] = okx ? ix : 0;
+        yv |= (oky ? 1u : 0u) << t;
+        xv |= (okx ? 1u : 0u) << t;
       }
-    } else {
-      a_n[i] = 0;
-      a_y[i] = -(1 << 28);
-      a_x[i] = -(1 << 28);
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+        for (int tx = 0; tx < 3; ++tx)
+          if (((yv >> ty) & 1u) && ((xv >> tx) & 1u)) vmask[j] |= 1u << (ty * p.kw + tx);
     }
+    rt[j] = RowTab{yp[0], yp[1], yp[2], xp[0], xp[1], xp[2]};
+  }
+  const bf16* b_src[BP];
+  bool b_ok[BP];
+#pragma unroll
+  for (int j = 0; j < BP; ++j) {
+    const int row = (tid >> 3) + 32 * j;
+    const int co = n0 + row;
+    b_ok[j] = co < p.cout;
+    b_src[j] = p.w + (long)(b_ok[j] ? co : 0) * p.ktot + ((slot ^ (row & 7)) * 8);
   }
   const int cch = SMALLC ? 1 : (p.cin >> 6);
+  const bf16* zero = (const bf16*)g_zero_line;
 
-  uint4 ra[AP], rb[BP];
-
-  auto load_chunk = [&](int kc) {
-    int ky = 0, kx = 0, c = 0;
-    bool tap_ok = true;
+  auto issue = [&](int kc, int stage) {
+    DC_LDS char* sbase = (DC_LDS char*)smem + stage * STAGE;
     if (!SMALLC) {
+      // the whole 64-channel chunk sits in one tap and one source (c1 % 64 == 0): uniform scalars;
+      // the tap is dispatched to a compile-time (ky, kx) so the row tables stay in registers
       const int tap = kc / cch;
-      c = (kc - tap * cch) * 64 + piece * 8;
-      ky = tap / p.kw;
-      kx = tap - ky * p.kw;
+      const int c0 = (kc - tap * cch) * 64;
+      const bool second = c0 >= p.c1;
+      const bf16* base = second ? p.x2 + (c0 - p.c1) : p.x + c0;
+      const int ld = second ? p.ldx2 : p.ldx;
+      auto gather = [&](auto KY, auto KX) {
+        constexpr int ky = decltype(KY)::value, kx = decltype(KX)::value;
+        constexpr int t = ky * 3 + kx;
+#pragma unroll
+        for (int j = 0; j < AP; ++j) {
+          const int yy = ky == 0 ? rt[j].y0 : (ky == 1 ? rt[j].y1 : rt[j].y2);
+          const int xx = kx == 0 ? rt[j].x0 : (kx == 1 ? rt[j].x1 : rt[j].x2);
+          const bool ok = (vmask[j] >> (p.kw == 3 ? t : 0)) & 1u;
+          const bf16* src = ok ? base + (long)(yy + xx) * ld + a_sw[j] * 8 : zero;
+          __builtin_amdgcn_global_load_lds((const void*)src, sbase + (wid * 64 + 256 * j) * 16, 16, 0, 0);
+        }
+      };
+      using Z = std::integral_constant<int, 0>;
+      using O = std::integral_constant<int, 1>;
+      using T = std::integral_constant<int, 2>;
+      switch (p.kw == 3 ? tap : 0) {
+        case 0: gather(Z{}, Z{}); break;
+        case 1: gather(Z{}, O{}); break;
+        case 2: gather(Z{}, T{}); break;
+        case 3: gather(O{}, Z{}); break;
+        case 4: gather(O{}, O{}); break;
+        case 5: gather(O{}, T{}); break;
+        case 6: gather(T{}, Z{}); break;
+        case 7: gather(T{}, O{}); break;
+        default: gather(T{}, T{}); break;
+      }
     } else {
-      const int k = kc * 64 + piece * 8;
-      const int tap = k / p.cin;
-      c = k - tap * p.cin;
-      tap_ok = tap < p.kh * p.kw;
-      ky = tap / p.kw;
-      kx = tap - ky * p.kw;
-    }
 #pragma unroll
-    for (int i = 0; i < AP; ++i) {
-      int iy = a_y[i] + ky, ix = a_x[i] + kx;
-      bool ok = tap_ok;
-      if (p.mode == 0) {
-        ok = ok && iy >= 0 && iy < p.hin && ix >= 0 && ix < p.win;
-      } else if (p.mode == 1) {
-        ok = ok && iy >= 0 && iy < p.hout && ix >= 0 && ix < p.wout;
-        iy = (int)(((long)iy * p.hin) / p.hout);
-        ix = (int)(((long)ix * p.win) / p.wout);
-      } else {
-        ok = ok && iy >= 0 && ix >= 0 && !(iy & 1) && !(ix & 1);
-        iy >>= 1;
-        ix >>= 1;
-        ok = ok && iy < p.hin && ix < p.win;
+      for (int j = 0; j < AP; ++j) {
+        const int k = kc * 64 + a_sw[j] * 8;
+        const int tap = k / p.cin;
+        const int c = k - tap * p.cin;
+        const int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
+        const bool ok = tap < p.kh * p.kw && ((vmask[j] >> tap) & 1u);
+        const int pix = (ky == 0 ? rt[j].y0 : (ky == 1 ? rt[j].y1 : rt[j].y2)) +
+                        (kx == 0 ? rt[j].x0 : (kx == 1 ? rt[j].x1 : rt[j].x2));
+        const bf16* src = ok ? p.x + (long)pix * p.ldx + c : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, sbase + (wid * 64 + 256 * j) * 16, 16, 0, 0);
       }
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ok) {
-        const long pix = ((long)a_n[i] * p.hin + iy) * p.win + ix;
-        const bf16* src = (c < p.c1) ? (p.x + pix * p.ldx + c) : (p.x2 + pix * p.ldx2 + (c - p.c1));
-        v = *reinterpret_cast<const uint4*>(src);
-      }
-      ra[i] = v;
     }
 #pragma unroll
     for (int j = 0; j < BP; ++j) {
-      const int co = n0 + (tid >> 3) + 32 * j;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (co < p.cout) v = *reinterpret_cast<const uint4*>(p.w + (long)co * p.ktot + kc * 64 + piece * 8);
-      rb[j] = v;
-    }
-  };
-
-  auto store_chunk = [&](int stage) {
-    char* sa = smem + stage * Smem<BM, BN>::STAGE;
-    char* sb = sa + BM * 128;
-#pragma unroll
-    for (int i = 0; i < AP; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(sa + row * 128 + ((piece ^ (row & 7)) << 4)) = ra[i];
-    }
-#pragma unroll
-    for (int j = 0; j < BP; ++j) {
-      const int row = (tid >> 3) + 32 * j;
-      *reinterpret_cast<uint4*>(sb + row * 128 + ((piece ^ (row & 7)) << 4)) = rb[j];
+      const void* src = b_ok[j] ? (const void*)(b_src[j] + kc * 64) : (const void*)zero;
+      __builtin_amdgcn_global_load_lds(src, sbase + BM * 128 + (wid * 64 + 256 * j) * 16, 16, 0, 0);
     }
   };
 
@@ -218,40 +284,40 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (kc_begin < kc_end) {
-    load_chunk(kc_begin);
-    store_chunk(0);
-  }
-  __syncthreads();
-  for (int kc = kc_begin; kc < kc_end; ++kc) {
-    const int cur = (kc - kc_begin) & 1;
-    const bool more = kc + 1 < kc_end;
-    if (more) load_chunk(kc + 1);
-    const char* sa = smem + cur * Smem<BM, BN>::STAGE;
+  for (int s = 0; s < S - 1 && s < nkc; ++s) issue(kc_begin + s, s);
+  for (int i = 0; i < nkc; ++i) {
+    wait_chunks<L, S>(min(S - 2, nkc - 1 - i));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (i + S - 1 < nkc) issue(kc_begin + i + S - 1, (i + S - 1) % S);
+    const char* sa = smem + (i % S) * STAGE;
     const char* sb = sa + BM * 128;
+    bf16x8 af[2][MI], bfr[2][NJ];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
-      bf16x8 af[MI], bfr[NJ];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int row = wm * WM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(sa + row * 128 + ((chunk ^ (row & 7)) << 4));
+      for (int ii = 0; ii < MI; ++ii) {
+        const int row = wm * WM + ii * 16 + (lane & 15);
+        af[ks][ii] = *reinterpret_cast<const bf16x8*>(sa + row * 128 + ((chunk ^ (row & 7)) << 4));
       }
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int row = wn * WN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(sb + row * 128 + ((chunk ^ (row & 7)) << 4));
+      for (int jj = 0; jj < NJ; ++jj) {
+        const int row = wn * WN + jj * 16 + (lane & 15);
+        bfr[ks][jj] = *reinterpret_cast<const bf16x8*>(sb + row * 128 + ((chunk ^ (row & 7)) << 4));
       }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store_chunk(cur ^ 1);
-    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj)
+          acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][ii], bfr[ks][jj], acc[ii][jj], 0, 0, 0);
   }
+  vm_wait<0>();
+  __syncthreads();
 
   // ---- epilogue: accumulators -> LDS fp32 tile -> 8-wide coalesced rows
   float* cs = reinterpret_cast<float*>(smem);
@@ -307,23 +373,28 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvGemmParams
   }
 }
 
-template <int BM, int BN, bool SMALLC>
-int launch_tile(ConvGemmParams& p, long M, hipStream_t stream) {
+// algorithm table: tile (BM, BN) and ring depth S
+struct Algo {
+  int bm, bn, s;
+};
+constexpr Algo kAlgos[] = {{0, 0, 0}, {128, 128, 4}, {128, 64, 5}, {64, 64, 4}, {64, 128, 4}, {128, 128, 3}};
+constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
+
+template <int BM, int BN, int S>
+int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t stream) {
   const int tiles = (int)((M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
   const int nk = p.ktot / 64;
   p.npad = ((p.cout + BN - 1) / BN) * BN;
-  int splits = 1;
-  if (p.ws != nullptr && tiles < 200 && nk >= 8) {
-    splits = (400 + tiles - 1) / tiles;
-    splits = min(splits, nk / 4);
-    splits = min(splits, 16);
-    while (splits > 1 && (long)splits * M * p.npad * 4 > p.ws_bytes) --splits;
-    splits = max(splits, 1);
-  }
+  splits = max(1, min(splits, nk));
+  if (p.ws == nullptr) splits = 1;
+  while (splits > 1 && (long)splits * M * p.npad * 4 > p.ws_bytes) --splits;
   p.kps = (nk + splits - 1) / splits;
   splits = (nk + p.kps - 1) / p.kps;
   p.splits = splits;
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, SMALLC>), dim3(tiles, splits), dim3(256), 0, stream, p);
+  if (smallc)
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, S, true>), dim3(tiles, splits), dim3(256), 0, stream, p);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, S, false>), dim3(tiles, splits), dim3(256), 0, stream, p);
   if (splits > 1) {
     const long groups = M * (p.npad / 8);
     const long nbl = (groups + 255) / 256;
@@ -334,9 +405,26 @@ int launch_tile(ConvGemmParams& p, long M, hipStream_t stream) {
   return DC_OK;
 }
 
+// heuristic when the caller does not choose: enough work units for the 256 CUs
+void auto_algo(long M, int cout, int nk, int& algo, int& splits) {
+  auto units = [&](int bm, int bn) { return (int)((M + bm - 1) / bm) * ((cout + bn - 1) / bn); };
+  const bool narrow = (cout <= 64) || (((cout + 63) / 64) * 64 < ((cout + 127) / 128) * 128);
+  if (!narrow && units(128, 128) >= 192) {
+    algo = 1;
+  } else if (units(128, 64) >= 160) {
+    algo = 2;
+  } else {
+    algo = (M <= 64 && !narrow) ? 4 : 3;
+  }
+  const Algo a = kAlgos[algo];
+  const int u = units(a.bm, a.bn);
+  splits = 1;
+  if (u < 160 && nk >= 8) splits = min(min((320 + u - 1) / u, nk / 4), 16);
+}
+
 }  // namespace
 
-#include "../../include/dcamd.h"
+extern "C" int dc_conv_num_algos(void) { return kNumAlgos; }
 
 extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (!d || !d->x || !d->w || !d->y) return DC_ERR_ARG;
@@ -364,6 +452,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
+  if (d->algo < 0 || d->algo > kNumAlgos || d->splitk < 0) return DC_ERR_ARG;
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;
@@ -373,9 +462,19 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (((uintptr_t)p.resid | (uintptr_t)p.mask) & 15) return DC_ERR_ALIGN;
   const long M = (long)p.nb * p.hout * p.wout;
   hipStream_t s = (hipStream_t)stream;
-  const bool narrow = (p.cout <= 64) || (((p.cout + 63) / 64) * 64 < ((p.cout + 127) / 128) * 128);
-  if (smallc) {
-    return narrow ? launch_tile<128, 64, true>(p, M, s) : launch_tile<128, 128, true>(p, M, s);
+  int algo = d->algo, splits = d->splitk;
+  if (algo == 0 || splits == 0) {
+    int a2, s2;
+    auto_algo(M, p.cout, p.ktot / 64, a2, s2);
+    if (algo == 0) algo = a2;
+    if (splits == 0) splits = (d->algo == 0) ? s2 : 1;
   }
-  return narrow ? launch_tile<128, 64, false>(p, M, s) : launch_tile<128, 128, false>(p, M, s);
+  switch (algo) {
+    case 1: return launch_algo<128, 128, 4>(p, M, splits, smallc, s);
+    case 2: return launch_algo<128, 64, 5>(p, M, splits, smallc, s);
+    case 3: return launch_algo<64, 64, 4>(p, M, splits, smallc, s);
+    case 4: return launch_algo<64, 128, 4>(p, M, splits, smallc, s);
+    case 5: return launch_algo<128, 128, 3>(p, M, splits, smallc, s);
+    default: return DC_ERR_ARG;
+  }
 }

@@ -57,6 +57,12 @@ class Ctx:
         self.device = torch.device(device)
         self.ws = torch.empty(ws_mb * (1 << 20) // 4, dtype=torch.float32, device=self.device)
         self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.algo_cache: dict = {}
+        self.tune = False   # plan-time autotuning of dc_conv_gemm variants (see choose_algo)
+
+    def choose_algo(self, d):
+        """(algo, splitk) for a conv descriptor: cached autotune result, else the library heuristic."""
+        return self.algo_cache.get(conv_key(d), (0, 0))
 
     @property
     def stream(self) -> int:
@@ -70,10 +76,14 @@ class Ctx:
 
 
 # ------------------------------------------------------------------------- conv / linear
+def conv_key(d) -> tuple:
+    return (d.mode, d.nb, d.hin, d.win, d.cin, d.hout, d.wout, d.cout, d.kh, d.stride, bool(d.x2), d.ktot)
+
+
 def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin: int, hout: int, wout: int,
               cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
               c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
-              y=None, splitk: bool = True):
+              y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None):
     d = ConvDesc()
     d.x = P(x)
     d.ldx = LD(x)
@@ -98,6 +108,10 @@ def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     d.ldy = LD(y)
     d.ws = ctx.ws.data_ptr() if splitk else None
     d.ws_bytes = ctx.ws_bytes if splitk else 0
+    if algo is None:
+        algo, nsplit = ctx.choose_algo(d)
+    d.algo = algo
+    d.splitk = nsplit or 0
     call("dc_conv_gemm", C.byref(d), ctx.stream)
     return y
 

@@ -52,8 +52,11 @@ typedef struct dc_conv_desc {
   int ldy;
   float* ws;       /* split-K workspace (may be NULL: no split-K) */
   long long ws_bytes;
+  int algo;        /* 0 = heuristic, 1..dc_conv_num_algos(): tile/ring variant (plan-time autotuned) */
+  int splitk;      /* 0 = heuristic, >=1 explicit K split (needs ws) */
 } dc_conv_desc;
 
+int dc_conv_num_algos(void);
 int dc_conv_gemm(const dc_conv_desc* d, void* stream);
 
 /* ---------------------------------------------------------------- normalisation

@@ -286,3 +286,32 @@ def test_geglu_and_upsample_adjoint(ctx):
         ops.upsample_adjoint(ctx, nhwc(g), 2, hh_, wh, 64, hl, wl, out)
         torch.cuda.synchronize()
         assert rel(nchw(out, 2, hl, wl), x.grad) < 1e-2
+
+
+@pytest.mark.parametrize("algo", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("nsplit", [1, 3])
+def test_conv_all_algos(ctx, algo, nsplit):
+    """every tile / ring variant and split-K on conv (incl. concat, stride 2, upsample) and linear."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    cases = [(2, 128, 64, 192, 9, 10, 1, 0), (1, 64, 0, 128, 12, 8, 2, 0), (1, 64, 0, 64, 5, 7, 1, 1),
+             (1, 320, 0, 320, 1, 200, 1, 0)]
+    for n, c1, c2, cout, h, w, stride, mode in cases:
+        cin = c1 + c2
+        xa = rnd(n, c1, h, w, seed=40)
+        xb = rnd(n, c2, h, w, seed=41) if c2 else None
+        k = 1 if (h == 1 and cin == 320) else 3
+        wt = rnd(cout, cin, k, k, scale=1 / math.sqrt(cin * k * k), seed=42)
+        xin = torch.cat([xa, xb], 1) if c2 else xa
+        if mode == 1:
+            ho, wo = 2 * h, 2 * w
+            ref = F.conv2d(F.interpolate(xin, size=(ho, wo), mode="nearest"), wt, padding=1)
+        else:
+            ref = F.conv2d(xin, wt, stride=stride, padding=k // 2)
+            ho, wo = ref.shape[-2:]
+        y = torch.empty(n * ho * wo, cout, dtype=torch.bfloat16, device=dev)
+        ops.conv_gemm(ctx, nhwc(xa), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=h, win=w, cin=cin, hout=ho,
+                      wout=wo, cout=cout, kh=k, kw=k, stride=stride, pad=k // 2, mode=mode,
+                      x2=nhwc(xb) if c2 else None, c1=c1 if c2 else 0, y=y, algo=algo, nsplit=nsplit)
+        torch.cuda.synchronize()
+        assert rel(nchw(y, n, ho, wo), ref) < 1e-2, (algo, nsplit, n, cin, cout, h, w, stride, mode)

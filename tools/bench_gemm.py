@@ -52,23 +52,29 @@ def main():
         y = torch.empty(nb * ho * wo, cout, device=dev, dtype=torch.bfloat16)
         b = torch.zeros(cout, device=dev)
 
-        def run():
-            ops.conv_gemm(ctx, x, wt, nb=nb, hin=hin, win=win, cin=cin, hout=ho, wout=wo, cout=cout, kh=k, kw=k,
-                          stride=stride, pad=k // 2, mode=mode, bias=b, y=y)
-
-        for _ in range(3):
-            run()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.reps):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / args.reps
         flops = 2.0 * nb * ho * wo * cout * k * k * cin
-        print(f"{name:18s} M={nb*ho*wo:7d} N={cout:6d} K={k*k*cin:6d}  {ms*1e3:9.1f} us  {flops/ms/1e9:8.1f} TFLOP/s",
-              flush=True)
+        res = []
+        for algo, ns in [(0, 0)] + [(a, s) for a in range(1, 6) for s in (1, 2, 4, 8)]:
+            def run():
+                ops.conv_gemm(ctx, x, wt, nb=nb, hin=hin, win=win, cin=cin, hout=ho, wout=wo, cout=cout, kh=k,
+                              kw=k, stride=stride, pad=k // 2, mode=mode, bias=b, y=y, algo=algo, nsplit=ns)
+
+            for _ in range(2):
+                run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / args.reps
+            res.append((ms, algo, ns))
+        auto_ms = res[0][0]
+        best = min(res)
+        print(f"{name:18s} M={nb*ho*wo:7d} N={cout:6d} K={k*k*cin:6d}  auto {auto_ms*1e3:8.1f} us "
+              f"{flops/auto_ms/1e9:7.1f} TF | best algo {best[1]} split {best[2]} {best[0]*1e3:8.1f} us "
+              f"{flops/best[0]/1e9:7.1f} TF", flush=True)
 
 
 if __name__ == "__main__":
