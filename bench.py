@@ -138,12 +138,14 @@ def main():
     from depth_completion_amd import synthetic
     from depth_completion_amd.config import MARIGOLD_V1
     from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    from depth_completion_amd.shard import frame_shard, max_over_ranks
 
     pipe = MarigoldDepthCompletionPipeline(synthetic.unet_state_dict(MARIGOLD_V1, 11), synthetic.taesd_state_dict(12),
                                            synthetic.text_embedding(13, 1024), device=dev,
                                            use_graph=not args.no_graph)
     B, H, W = args.batch, args.height, args.width
-    frames = [synth_frame(H, W, args.points, seed=rank * 100003 + i) for i in range(B)]
+    # the job's frames 0..world*B-1, contiguous shard per rank (depth_completion_amd/shard.py)
+    frames = [synth_frame(H, W, args.points, seed=i) for i in frame_shard(world * B, rank, world)]
     imgs = torch.stack([f[0] for f in frames]).to(dev)
     sps = torch.stack([f[1] for f in frames]).to(dev)
     kw = dict(norm="const", steps=args.denoise_steps, resolution=768)
@@ -160,10 +162,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device=dev)
     assert torch.isfinite(dense).all(), "non-finite dense output"
 
     frames_total = world * args.steps * B

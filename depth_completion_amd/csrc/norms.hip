@@ -79,9 +79,12 @@ __global__ void gn_stats_kernel(GNShape s, float* part) {
 // one block per frame, one wave per group (looping): fp64 fold of the chunk partials.
 // mode 0: out = (mean, rstd) from (sum, sumsq); mode 1: out = (sum a / cnt, sum b / cnt)
 __global__ void gn_finalize_kernel(GNShape s, const float* part, float eps, int mode, float* out) {
-  const int n = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // one wave per (frame, group): grid (ceil(groups / 4), nb) x 256 threads
+  const int n = blockIdx.y, lane = threadIdx.x & 63;
   const double cnt = (double)s.hw * s.cpg;
-  for (int g = wid; g < s.groups; g += nw) {
+  {
+    const int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (g >= s.groups) return;
     double ta = 0.0, tb = 0.0;
     for (int k = lane; k < s.nchunk; k += 64) {
       const float* src = part + (((long)n * s.nchunk + k) * s.groups + g) * 2;
@@ -256,7 +259,7 @@ extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2
   const int threads = s.cgs * s.R;
   const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
   hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nb), dim3(256), 0, st, s, ws, eps, 0, stats);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, eps, 0, stats);
   hipLaunchKernelGGL(gn_apply_kernel, ew_grid((long)nb * hw * s.cgs), dim3(256), 0, st, s, stats, gamma, beta, silu,
                      (bf16*)y, ldy);
   DC_CHECK_LAUNCH();
@@ -276,7 +279,7 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   float* ab = ws + gn_part_floats(s);
   hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, stats, gamma, beta, silu,
                      (const bf16*)dy, lddy, ws);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3(nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
   hipLaunchKernelGGL(gn_bwd_apply_kernel, ew_grid((long)nb * hw * s.cgs), dim3(256), 0, st, s, stats, gamma, beta,
                      silu, (const bf16*)dy, lddy, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1,
                      (const bf16*)add2, ldadd2);

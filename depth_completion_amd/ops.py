@@ -7,7 +7,10 @@ PyTorch is used only for device memory and the current stream handle.
 from __future__ import annotations
 
 import ctypes as C
+import json
+import os
 from dataclasses import dataclass
+from pathlib import Path
 
 import torch
 
@@ -50,19 +53,44 @@ def LD(t) -> int:
     return t.ld if isinstance(t, Slice) else t.shape[-1]
 
 
-class Ctx:
-    """Execution context: stream, fp32 scratch workspace and the device step counter."""
+TUNED_TABLE = Path(__file__).resolve().parent / "tuned_gfx950.json"
 
-    def __init__(self, device, ws_mb: int = 96):
+
+def load_tuned(path: Path = TUNED_TABLE) -> dict:
+    """Committed (algo, splitk) choices per conv shape, measured on MI355X by tools/tune_gemm.py."""
+    if not path.exists():
+        return {}
+    return {tuple(e["key"]): (e["algo"], e["splitk"]) for e in json.loads(path.read_text())}
+
+
+def save_tuned(cache: dict, path) -> None:
+    ent = [{"key": list(k), "algo": a, "splitk": s} for k, (a, s) in sorted(cache.items())]
+    Path(path).write_text(json.dumps(ent, indent=0))
+
+
+class Ctx:
+    """Execution context: stream, fp32 scratch workspace and the device step counter.
+
+    ``algo_cache`` maps a conv shape key to the (tile algo, split-K) variant of dc_conv_gemm; it
+    starts from the committed tuned table.  With ``tune`` (env DC_TUNE=1) a shape missing from
+    the cache is timed over every variant on the call's own operands the first time it runs
+    eagerly (never while a hipGraph is being captured); otherwise the library heuristic runs.
+    """
+
+    def __init__(self, device, ws_mb: int = 96, tune: bool | None = None):
         self.device = torch.device(device)
         self.ws = torch.empty(ws_mb * (1 << 20) // 4, dtype=torch.float32, device=self.device)
         self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.algo_cache: dict = {}
-        self.tune = False   # plan-time autotuning of dc_conv_gemm variants (see choose_algo)
+        self.algo_cache: dict = load_tuned()
+        self.tune = os.environ.get("DC_TUNE") == "1" if tune is None else tune
 
-    def choose_algo(self, d):
-        """(algo, splitk) for a conv descriptor: cached autotune result, else the library heuristic."""
-        return self.algo_cache.get(conv_key(d), (0, 0))
+    def choose_algo(self, d, y=None):
+        """(algo, splitk) for a conv descriptor: tuned table / autotune, else the library heuristic."""
+        key = conv_key(d)
+        if key not in self.algo_cache and self.tune and self.device.type == "cuda" \
+                and not torch.cuda.is_current_stream_capturing():
+            self.algo_cache[key] = _autotune(self, d, y)
+        return self.algo_cache.get(key, (0, 0))
 
     @property
     def stream(self) -> int:
@@ -109,11 +137,42 @@ def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     d.ws = ctx.ws.data_ptr() if splitk else None
     d.ws_bytes = ctx.ws_bytes if splitk else 0
     if algo is None:
-        algo, nsplit = ctx.choose_algo(d)
+        algo, nsplit = ctx.choose_algo(d, y)
     d.algo = algo
     d.splitk = nsplit or 0
     call("dc_conv_gemm", C.byref(d), ctx.stream)
     return y
+
+
+def _autotune(ctx: Ctx, d, y, reps: int = 3) -> tuple:
+    """Time every (algo, splitk) variant of one conv on its own operands; returns the fastest.
+
+    Candidates write a scratch copy of the output so in-place epilogues (resid == y) stay intact.
+    """
+    rows = d.nb * d.hout * d.wout
+    tmp = torch.empty(rows, d.ldy, dtype=BF16, device=ctx.device)
+    base = y.t.data_ptr() if isinstance(y, Slice) else y.data_ptr()
+    dt = ConvDesc.from_buffer_copy(d)
+    dt.y = tmp.data_ptr() + (d.y - base)
+    nalg = _lib.load().dc_conv_num_algos()
+    cands = [(0, 0)] + [(a, s) for a in range(1, nalg + 1) for s in (1, 2, 4, 8)]
+    best, best_t = (0, 0), float("inf")
+    for a, s in cands:
+        dt.algo, dt.splitk = a, s
+        try:
+            call("dc_conv_gemm", C.byref(dt), ctx.stream)
+        except _lib.DCError:
+            continue
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            call("dc_conv_gemm", C.byref(dt), ctx.stream)
+        e1.record()
+        e1.synchronize()
+        t = e0.elapsed_time(e1)
+        if t < best_t * 0.97:  # prefer the earlier (heuristic / fewer splits) on near-ties
+            best, best_t = (a, s), t
+    return best
 
 
 def linear(ctx: Ctx, x, w: torch.Tensor, rows: int, cout: int, y, bias=None, resid=None, rowbias=None,

@@ -1,0 +1,47 @@
+"""Measure the fastest dc_conv_gemm variant for every conv/linear shape of the sampler (GPU).
+
+Runs one eager guided call per workload with Ctx.tune on (each new shape is timed over all tile
+algos x split-K on its real operands) and writes the table that ops.load_tuned() reads.
+
+Usage: python tools/tune_gemm.py [--batches 1 8] [--out depth_completion_amd/tuned_gfx950.json]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import synth_frame  # noqa: E402
+from depth_completion_amd import ops, synthetic  # noqa: E402
+from depth_completion_amd.config import MARIGOLD_V1  # noqa: E402
+from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", type=int, nargs="+", default=[1, 8])
+    ap.add_argument("--out", default="gpurun_out/tuned_gfx950.json")
+    ap.add_argument("--fresh", action="store_true", help="ignore the committed table")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    pipe = MarigoldDepthCompletionPipeline(synthetic.unet_state_dict(MARIGOLD_V1, 11), synthetic.taesd_state_dict(12),
+                                           synthetic.text_embedding(13, 1024), device=dev, use_graph=False)
+    if args.fresh:
+        pipe.ctx.algo_cache = {}
+    pipe.ctx.tune = True
+    for b in args.batches:
+        fr = [synth_frame(576, 768, 500, i) for i in range(b)]
+        imgs = torch.stack([f[0] for f in fr]).to(dev)
+        sps = torch.stack([f[1] for f in fr]).to(dev)
+        n0 = len(pipe.ctx.algo_cache)
+        pipe(imgs, sps, 120.0, norm="const", steps=2, resolution=768)
+        torch.cuda.synchronize()
+        print(f"batch {b}: {len(pipe.ctx.algo_cache) - n0} new shapes tuned", flush=True)
+    ops.save_tuned(pipe.ctx.algo_cache, args.out)
+    for k, v in sorted(pipe.ctx.algo_cache.items()):
+        print(k, v)
+
+
+if __name__ == "__main__":
+    main()
