@@ -74,6 +74,7 @@ def measure_conv_kernel(pipe, st):
 
     ops.call = wrapped
     try:
+        ops.memset(pipe.ctx, pipe.ctx.step)  # step index 0: per-step tables have exactly S rows
         pipe._step(st)
     finally:
         ops.call = orig

@@ -49,10 +49,10 @@ __device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of ever
 
 namespace {
 
-__device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, int c, float* v) {
+__device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, int c, float* v, bool add_bias) {
   const bool full = (c + 8 <= p.cout);
   const int cnt = full ? 8 : (p.cout - c);
-  if (p.bias) {
+  if (add_bias && p.bias) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) if (i < cnt) v[i] += p.bias[c + i];
   }
@@ -115,22 +115,38 @@ __device__ __forceinline__ void wait_chunks(int ahead) {
   }
 }
 
-template <int BM, int BN, int S>
+// LDS bytes: S ring stages of (BM + BN) rows x BK bf16, reused by the per-wave bf16 epilogue tile
+template <int BM, int BN, int BK, int S>
 struct Cfg {
-  static constexpr int STAGE = (BM + BN) * 128;
-  static constexpr int EPI = BM * (BN + 4) * 4;
+  static constexpr int RB = BK * 2;                                     // bytes per tile row per stage
+  static constexpr int STAGE = (BM + BN) * RB;
+  static constexpr int EPI = 4 * (BM / 2) * (BN / 2 + 8) * 2;          // 4 waves x [WM][WN+8] bf16
   static constexpr int LDS = (S * STAGE > EPI) ? S * STAGE : EPI;
 };
 
-template <int BM, int BN, int S, bool SMALLC>
+// XOR swizzle of the 16-B chunk index within a tile row, chosen so that the ds_read_b128 fragment
+// reads (16 consecutive rows x 4 chunks per instruction, lanes grouped 0-3/12-15/20-27 ... by the
+// LDS crossbar) are conflict-free: BK=64 rows are 8 chunks (128 B) wide, BK=32 rows 4 chunks.
+template <int BK>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (BK == 64) return row & 7;
+  else return ((row >> 3) & 1) << 1;
+}
+
+template <int BM, int BN, int BK, int S, bool SMALLC>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) {
-  constexpr int AP = BM / 32;  // A pieces (16 B) per thread per k-chunk
-  constexpr int BP = BN / 32;
-  constexpr int L = AP + BP;   // LDS-DMA instructions per thread per k-chunk
+  constexpr int CPR = BK / 8;            // 16-B chunks per tile row
+  constexpr int RPI = 256 / CPR;         // tile rows covered by one block-wide LDS-DMA instruction
+  constexpr int AP = BM / RPI;           // A pieces (16 B) per thread per k-chunk
+  constexpr int BP = BN / RPI;
+  constexpr int L = AP + BP;             // LDS-DMA instructions per thread per k-chunk
+  constexpr int KS = BK / 32;            // MFMA k-steps per chunk
+  constexpr int RB = Cfg<BM, BN, BK, S>::RB;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
-  constexpr int STAGE = Cfg<BM, BN, S>::STAGE;
-  __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, S>::LDS];
+  constexpr int STAGE = Cfg<BM, BN, BK, S>::STAGE;
+  static_assert(AP >= 1 && BP >= 1, "tile too small for the block-wide DMA");
+  __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, BK, S>::LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -146,14 +162,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   const long m0 = (long)tm * BM;
   const int n0 = tn * BN;
 
-  const int nk = p.ktot >> 6;
+  const int nk = p.ktot / BK;
   const int kc_begin = blockIdx.y * p.kps;
   const int kc_end = min(nk, kc_begin + p.kps);
   const int nkc = max(0, kc_end - kc_begin);
 
-  // per-thread A-row gather tables (piece j covers tile row (tid>>3) + 32 j, slot tid&7):
+  // per-thread A-row gather tables (piece j covers tile row tid/CPR + RPI j, chunk slot tid%CPR):
   // source pixel = ypix[ky] + xpix[kx] for every mode (direct / upsample / transposed), valid-tap bitmask
-  const int slot = tid & 7;
+  const int slot = tid % CPR;
   struct RowTab {
     int y0, y1, y2, x0, x1, x2;
   };
@@ -162,8 +178,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   unsigned vmask[AP];
 #pragma unroll
   for (int j = 0; j < AP; ++j) {
-    const int row = (tid >> 3) + 32 * j;
-    a_sw[j] = slot ^ (row & 7);  // logical 16-B chunk this lane fetches (XOR swizzle via the source)
+    const int row = tid / CPR + RPI * j;
+    a_sw[j] = slot ^ swz<BK>(row);  // logical 16-B chunk this lane fetches (XOR swizzle via the source)
     const long m = m0 + row;
     vmask[j] = 0u;
     int yp[3] = {0, 0, 0}, xp[3] = {0, 0, 0};
@@ -213,21 +229,21 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   bool b_ok[BP];
 #pragma unroll
   for (int j = 0; j < BP; ++j) {
-    const int row = (tid >> 3) + 32 * j;
+    const int row = tid / CPR + RPI * j;
     const int co = n0 + row;
     b_ok[j] = co < p.cout;
-    b_src[j] = p.w + (long)(b_ok[j] ? co : 0) * p.ktot + ((slot ^ (row & 7)) * 8);
+    b_src[j] = p.w + (long)(b_ok[j] ? co : 0) * p.ktot + ((slot ^ swz<BK>(row)) * 8);
   }
-  const int cch = SMALLC ? 1 : (p.cin >> 6);
+  const int cch = SMALLC ? 1 : (p.cin / BK);
   const bf16* zero = (const bf16*)g_zero_line;
 
   auto issue = [&](int kc, int stage) {
     DC_LDS char* sbase = (DC_LDS char*)smem + stage * STAGE;
     if (!SMALLC) {
-      // the whole 64-channel chunk sits in one tap and one source (c1 % 64 == 0): uniform scalars;
+      // the whole BK-channel chunk sits in one tap and one source (c1 % 64 == 0): uniform scalars;
       // the tap is dispatched to a compile-time (ky, kx) so the row tables stay in registers
       const int tap = kc / cch;
-      const int c0 = (kc - tap * cch) * 64;
+      const int c0 = (kc - tap * cch) * BK;
       const bool second = c0 >= p.c1;
       const bf16* base = second ? p.x2 + (c0 - p.c1) : p.x + c0;
       const int ld = second ? p.ldx2 : p.ldx;
@@ -260,7 +276,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     } else {
 #pragma unroll
       for (int j = 0; j < AP; ++j) {
-        const int k = kc * 64 + a_sw[j] * 8;
+        const int k = kc * BK + a_sw[j] * 8;
         const int tap = k / p.cin;
         const int c = k - tap * p.cin;
         const int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
@@ -273,8 +289,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     }
 #pragma unroll
     for (int j = 0; j < BP; ++j) {
-      const void* src = b_ok[j] ? (const void*)(b_src[j] + kc * 64) : (const void*)zero;
-      __builtin_amdgcn_global_load_lds(src, sbase + BM * 128 + (wid * 64 + 256 * j) * 16, 16, 0, 0);
+      const void* src = b_ok[j] ? (const void*)(b_src[j] + kc * BK) : (const void*)zero;
+      __builtin_amdgcn_global_load_lds(src, sbase + BM * RB + (wid * 64 + 256 * j) * 16, 16, 0, 0);
     }
   };
 
@@ -292,24 +308,24 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     asm volatile("" ::: "memory");
     if (i + S - 1 < nkc) issue(kc_begin + i + S - 1, (i + S - 1) % S);
     const char* sa = smem + (i % S) * STAGE;
-    const char* sb = sa + BM * 128;
-    bf16x8 af[2][MI], bfr[2][NJ];
+    const char* sb = sa + BM * RB;
+    bf16x8 af[KS][MI], bfr[KS][NJ];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int ii = 0; ii < MI; ++ii) {
         const int row = wm * WM + ii * 16 + (lane & 15);
-        af[ks][ii] = *reinterpret_cast<const bf16x8*>(sa + row * 128 + ((chunk ^ (row & 7)) << 4));
+        af[ks][ii] = *reinterpret_cast<const bf16x8*>(sa + row * RB + ((chunk ^ swz<BK>(row)) << 4));
       }
 #pragma unroll
       for (int jj = 0; jj < NJ; ++jj) {
         const int row = wn * WN + jj * 16 + (lane & 15);
-        bfr[ks][jj] = *reinterpret_cast<const bf16x8*>(sb + row * 128 + ((chunk ^ (row & 7)) << 4));
+        bfr[ks][jj] = *reinterpret_cast<const bf16x8*>(sb + row * RB + ((chunk ^ swz<BK>(row)) << 4));
       }
     }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int ii = 0; ii < MI; ++ii)
 #pragma unroll
@@ -317,40 +333,48 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
           acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][ii], bfr[ks][jj], acc[ii][jj], 0, 0, 0);
   }
   vm_wait<0>();
-  __syncthreads();
 
-  // ---- epilogue: accumulators -> LDS fp32 tile -> 8-wide coalesced rows
-  float* cs = reinterpret_cast<float*>(smem);
-  constexpr int LDC = BN + 4;
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  if (p.splits > 1) {
+    // split-K: fp32 partial slab straight from the accumulators (16 lanes = 64 contiguous bytes)
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + e;
-        const int col = wn * WN + j * 16 + (lane & 15);
-        cs[row * LDC + col] = acc[i][j][e];
+        const long m = m0 + wm * WM + i * 16 + row_l + e;
+        if (m >= M) continue;
+        float* dst = p.ws + ((long)blockIdx.y * M + m) * p.npad + n0 + wn * WN + col_l;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) dst[j * 16] = acc[i][j][e];
       }
-  __syncthreads();
-  constexpr int GPR = BN / 8;
-  for (int g = tid; g < BM * GPR; g += 256) {
+    return;
+  }
+
+  // ---- epilogue: bias in fp32, round to bf16 into a per-wave LDS tile, then 16-B coalesced rows
+  __syncthreads();  // every wave is done reading the ring
+  constexpr int LDE = WN + 8;
+  bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = n0 + wn * WN + j * 16 + col_l;
+    const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) es[(i * 16 + row_l + e) * LDE + j * 16 + col_l] = (bf16)(acc[i][j][e] + bv);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  constexpr int GPR = WN / 8;
+#pragma unroll 4
+  for (int g = lane; g < WM * GPR; g += 64) {
     const int row = g / GPR, cg = g - (g / GPR) * GPR;
-    const long m = m0 + row;
-    const int c = n0 + cg * 8;
+    const long m = m0 + wm * WM + row;
+    const int c = n0 + wn * WN + cg * 8;
     if (m >= M || c >= p.cout) continue;
     float v[8];
-    const float4 lo = *reinterpret_cast<const float4*>(cs + row * LDC + cg * 8);
-    const float4 hi = *reinterpret_cast<const float4*>(cs + row * LDC + cg * 8 + 4);
-    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-    if (p.splits > 1) {
-      float* dst = p.ws + ((long)blockIdx.y * M + m) * p.npad + c;
-      *reinterpret_cast<float4*>(dst) = lo;
-      *reinterpret_cast<float4*>(dst + 4) = hi;
-    } else {
-      epilogue_store(p, m, c, v);
-    }
+    load8(es + row * LDE + cg * 8, v);
+    epilogue_store(p, m, c, v, false);
   }
 }
 
@@ -369,21 +393,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvGemmParams
       v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
       v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
     }
-    epilogue_store(p, m, c, v);
+    epilogue_store(p, m, c, v, true);
   }
 }
 
-// algorithm table: tile (BM, BN) and ring depth S
+// algorithm table: tile (BM, BN), k-chunk BK and ring depth S
 struct Algo {
-  int bm, bn, s;
+  int bm, bn, bk, s;
 };
-constexpr Algo kAlgos[] = {{0, 0, 0}, {128, 128, 4}, {128, 64, 5}, {64, 64, 4}, {64, 128, 4}, {128, 128, 3}};
+constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 5}, {64, 64, 64, 4},
+                           {64, 128, 64, 4},   {128, 128, 64, 3}, {128, 128, 32, 3}, {128, 64, 32, 4},
+                           {64, 64, 32, 4},    {256, 64, 32, 3},  {128, 128, 64, 2}};
 constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int BK, int S>
 int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t stream) {
   const int tiles = (int)((M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
-  const int nk = p.ktot / 64;
+  const int nk = p.ktot / BK;
   p.npad = ((p.cout + BN - 1) / BN) * BN;
   splits = max(1, min(splits, nk));
   if (p.ws == nullptr) splits = 1;
@@ -392,9 +418,9 @@ int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t 
   splits = (nk + p.kps - 1) / p.kps;
   p.splits = splits;
   if (smallc)
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, S, true>), dim3(tiles, splits), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true>), dim3(tiles, splits), dim3(256), 0, stream, p);
   else
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, S, false>), dim3(tiles, splits), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, false>), dim3(tiles, splits), dim3(256), 0, stream, p);
   if (splits > 1) {
     const long groups = M * (p.npad / 8);
     const long nbl = (groups + 255) / 256;
@@ -470,11 +496,10 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
     if (splits == 0) splits = (d->algo == 0) ? s2 : 1;
   }
   switch (algo) {
-    case 1: return launch_algo<128, 128, 4>(p, M, splits, smallc, s);
-    case 2: return launch_algo<128, 64, 5>(p, M, splits, smallc, s);
-    case 3: return launch_algo<64, 64, 4>(p, M, splits, smallc, s);
-    case 4: return launch_algo<64, 128, 4>(p, M, splits, smallc, s);
-    case 5: return launch_algo<128, 128, 3>(p, M, splits, smallc, s);
+#define DC_ALGO(i) \
+  case i: return launch_algo<kAlgos[i].bm, kAlgos[i].bn, kAlgos[i].bk, kAlgos[i].s>(p, M, splits, smallc, s);
+    DC_ALGO(1) DC_ALGO(2) DC_ALGO(3) DC_ALGO(4) DC_ALGO(5) DC_ALGO(6) DC_ALGO(7) DC_ALGO(8) DC_ALGO(9) DC_ALGO(10)
+#undef DC_ALGO
     default: return DC_ERR_ARG;
   }
 }
