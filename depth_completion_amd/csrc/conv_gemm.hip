@@ -403,7 +403,9 @@ struct Algo {
 };
 constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 5}, {64, 64, 64, 4},
                            {64, 128, 64, 4},   {128, 128, 64, 3}, {128, 128, 32, 3}, {128, 64, 32, 4},
-                           {64, 64, 32, 4},    {256, 64, 32, 3},  {128, 128, 64, 2}};
+                           {64, 64, 32, 4},    {256, 64, 32, 3},  {128, 128, 64, 2}, {128, 128, 32, 2},
+                           {128, 64, 64, 2},   {64, 64, 64, 2},   {256, 128, 32, 2}, {128, 256, 32, 2},
+                           {256, 64, 64, 2}};
 constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
 
 template <int BM, int BN, int BK, int S>
@@ -436,11 +438,11 @@ void auto_algo(long M, int cout, int nk, int& algo, int& splits) {
   auto units = [&](int bm, int bn) { return (int)((M + bm - 1) / bm) * ((cout + bn - 1) / bn); };
   const bool narrow = (cout <= 64) || (((cout + 63) / 64) * 64 < ((cout + 127) / 128) * 128);
   if (!narrow && units(128, 128) >= 192) {
-    algo = 1;
+    algo = 10;  // 128x128, BK 64, double-buffered (2 blocks / CU)
   } else if (units(128, 64) >= 160) {
-    algo = 2;
+    algo = 12;  // 128x64, BK 64, double-buffered
   } else {
-    algo = (M <= 64 && !narrow) ? 4 : 3;
+    algo = 13;  // 64x64, BK 64, double-buffered
   }
   const Algo a = kAlgos[algo];
   const int u = units(a.bm, a.bn);
@@ -499,6 +501,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
 #define DC_ALGO(i) \
   case i: return launch_algo<kAlgos[i].bm, kAlgos[i].bn, kAlgos[i].bk, kAlgos[i].s>(p, M, splits, smallc, s);
     DC_ALGO(1) DC_ALGO(2) DC_ALGO(3) DC_ALGO(4) DC_ALGO(5) DC_ALGO(6) DC_ALGO(7) DC_ALGO(8) DC_ALGO(9) DC_ALGO(10)
+    DC_ALGO(11) DC_ALGO(12) DC_ALGO(13) DC_ALGO(14) DC_ALGO(15) DC_ALGO(16)
 #undef DC_ALGO
     default: return DC_ERR_ARG;
   }
