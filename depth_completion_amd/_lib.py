@@ -9,7 +9,7 @@ import ctypes as C
 from pathlib import Path
 
 _LIB_PATH = Path(__file__).resolve().parent / "libdcamd.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -63,7 +63,7 @@ _SIGS = {
     "dc_sparse_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dc_decode_tail_bwd": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp],
     "dc_latent_update": [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
-    "dc_step_advance": [vp, vp],
+    "dc_step_advance": [vp, i32, vp],
     "dc_latent_init": [vp, vp, f32, i32, i32, vp, vp],
     "dc_final_dense": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],

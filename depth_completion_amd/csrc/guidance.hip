@@ -358,7 +358,11 @@ __global__ void latent_update_kernel(bf16* x8, const bf16* v, const bf16* gdir, 
   }
 }
 
-__global__ void step_advance_kernel(int* step) { *step += 1; }
+// saturates at the last table row, so replays past the end of a call never index beyond [S]
+__global__ void step_advance_kernel(int* step, int nsteps) {
+  const int s = *step + 1;
+  *step = s < nsteps ? s : nsteps - 1;
+}
 
 // initial depth latents (marigold_dc.py:677-704): noise [1][4][hw] (NCHW, repeated over frames),
 // optional warm start beta*noise + (1-beta)*prev (prev [nb][4][hw]) -> x8[...,4:8]
@@ -460,9 +464,9 @@ extern "C" int dc_latent_update(void* x8, const void* v, const void* gdir, const
   return DC_OK;
 }
 
-extern "C" int dc_step_advance(int* step, void* stream) {
-  if (!step) return DC_ERR_ARG;
-  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step);
+extern "C" int dc_step_advance(int* step, int nsteps, void* stream) {
+  if (!step || nsteps <= 0) return DC_ERR_ARG;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, step, nsteps);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

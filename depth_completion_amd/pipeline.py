@@ -341,4 +341,4 @@ class MarigoldDepthCompletionPipeline:
                   h * w, cs["coef"].data_ptr(), cs["adam"].data_ptr(), step, st["eps_norm"].data_ptr(),
                   st["m_lat"].data_ptr(), st["v_lat"].data_ptr(), st["affine"].data_ptr(), st["m_aff"].data_ptr(),
                   st["v_aff"].data_ptr(), st["daff"].data_ptr(), st["dbg"].data_ptr(), s)
-        _lib.call("dc_step_advance", step, s)
+        _lib.call("dc_step_advance", step, int(cs["coef"].shape[0]), s)

@@ -133,7 +133,7 @@ int dc_decode_tail_bwd(const void* dec_out, int ldo, const float* dA, int nb, in
 int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gunet, int nb, int hw, const float* coef,
                      const float* adam_tab, const int* step, const float* eps_norm, void* m_lat, void* v_lat,
                      float* affine, float* m_aff, float* v_aff, const float* daff_grad, float* dbg, void* stream);
-int dc_step_advance(int* step, void* stream);
+int dc_step_advance(int* step, int nsteps, void* stream);  /* saturates at nsteps-1 */
 int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8, void* stream);
 int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
                    const float* params, const float* affine, float* dense, void* stream);

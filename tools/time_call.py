@@ -41,6 +41,7 @@ def main():
 
     st = pipe._plans[(args.batch, pipe._call_state["h"], pipe._call_state["w"])]
     g = st["graph"]
+    pipe.ctx.step.zero_()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(50):
@@ -58,7 +59,8 @@ def main():
     t_eager = e0.elapsed_time(e1)
 
     print(f"full call {t_call*1e3:.1f} ms | 50 graph replays {t_graph*1e3:.1f} ms (host enqueue {t_host*1e3:.1f} ms)"
-          f" -> {t_graph/50*1e3:.2f} ms/step | eager step {t_eager:.2f} ms | per-call overhead ~{(t_call - t_graph)*1e3:.1f} ms")
+          f" -> {t_graph / 50 * 1e3:.2f} ms/step | eager step {t_eager:.2f} ms | per-call overhead "
+          f"~{(t_call - t_graph) * 1e3:.1f} ms", flush=True)
 
 
 if __name__ == "__main__":
