@@ -59,8 +59,8 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16* p, bool ok, float scale)
 }
 
 // stage a [64 rows][64 cols] bf16 tile (rows r0.., column offset col) into LDS with `stride`
-__device__ __forceinline__ void stage_load(const bf16* base, long ld, int r0, int rows_total, int col, uint4 (&reg)[2]) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ void stage_load(const bf16* base, long ld, int r0, int rows_total, int col, uint4 (&reg)[2],
+                                           int t) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (t >> 3) + 32 * i, piece = t & 7;
@@ -69,8 +69,7 @@ __device__ __forceinline__ void stage_load(const bf16* base, long ld, int r0, in
     reg[i] = v;
   }
 }
-__device__ __forceinline__ void stage_store(bf16* tile, int stride, const uint4 (&reg)[2], float scale) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ void stage_store(bf16* tile, int stride, const uint4 (&reg)[2], float scale, int t) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (t >> 3) + 32 * i, piece = t & 7;
@@ -86,11 +85,25 @@ __device__ __forceinline__ void stage_store(bf16* tile, int stride, const uint4 
 }
 
 // ------------------------------------------------------------------------------ forward
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo,
-                                                       float* lse) {
-  __shared__ __attribute__((aligned(16))) bf16 ks[2][64 * KSTR];
-  __shared__ __attribute__((aligned(16))) bf16 vs[2][64 * VSTR];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+// KS key-splits per block: waves 4p..4p+3 sweep the p-th contiguous range of key tiles for the same
+// 128 queries (KS x 4 waves per CU hide MFMA / softmax / LDS latency at small T x heads), then the
+// partial (m, l, O) are merged through LDS in a fixed order (deterministic).
+template <int KS>
+struct FwdLds {
+  static constexpr int K_BYTES = KS * 2 * 64 * KSTR * 2;
+  static constexpr int V_BYTES = KS * 2 * 64 * VSTR * 2;
+  static constexpr int RED = (KS - 1) * 4 * 34 * 64 * 4;
+  static constexpr int BYTES = (K_BYTES + V_BYTES > RED) ? K_BYTES + V_BYTES : RED;
+};
+
+template <int KS>
+__global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(const bf16* qkv, int ld, int T, int heads, bf16* o,
+                                                            int ldo, float* lse) {
+  __shared__ __attribute__((aligned(16))) char smem[FwdLds<KS>::BYTES];
+  const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) & 3, part = threadIdx.x >> 8, hh = lane >> 5;
+  const int lt = threadIdx.x & 255;
+  bf16* ks = reinterpret_cast<bf16*>(smem) + part * 2 * 64 * KSTR;
+  bf16* vs = reinterpret_cast<bf16*>(smem + FwdLds<KS>::K_BYTES) + part * 2 * 64 * VSTR;
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
@@ -108,79 +121,115 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* qkv, int ld, 
     for (int r = 0; r < 16; ++r) oacc[db][r] = 0.0f;
 
   const int ntiles = (T + 63) / 64;
+  const int per = (ntiles + KS - 1) / KS;
+  const int tb = part * per;
+  const int mine = max(0, min(ntiles, tb + per) - tb);
   uint4 rk[2], rv[2];
-  stage_load(base, ld, 0, T, C + h * 64, rk);
-  stage_load(base, ld, 0, T, 2 * C + h * 64, rv);
-  stage_store(ks[0], KSTR, rk, 1.0f);
-  stage_store(vs[0], VSTR, rv, 1.0f);
+  if (mine > 0) {
+    stage_load(base, ld, tb * 64, T, C + h * 64, rk, lt);
+    stage_load(base, ld, tb * 64, T, 2 * C + h * 64, rv, lt);
+    stage_store(ks, KSTR, rk, 1.0f, lt);
+    stage_store(vs, VSTR, rv, 1.0f, lt);
+  }
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < ntiles;
+  for (int i = 0; i < per; ++i) {
+    const int kt = tb + i;
+    const int cur = i & 1;
+    const bool more = i + 1 < mine;
     if (more) {
-      stage_load(base, ld, (kt + 1) * 64, T, C + h * 64, rk);
-      stage_load(base, ld, (kt + 1) * 64, T, 2 * C + h * 64, rv);
+      stage_load(base, ld, (kt + 1) * 64, T, C + h * 64, rk, lt);
+      stage_load(base, ld, (kt + 1) * 64, T, 2 * C + h * 64, rv, lt);
     }
-    const bf16* kt_s = ks[cur];
-    const bf16* vt_s = vs[cur];
-    f32x16 sacc[2];
+    if (i < mine) {
+      const bf16* kt_s = ks + cur * 64 * KSTR;
+      const bf16* vt_s = vs + cur * 64 * VSTR;
+      f32x16 sacc[2];
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
+      for (int b = 0; b < 2; ++b) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
+        for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+          sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[b], 0, 0, 0);
+        }
+      }
+      // scores -> log2 domain, mask keys beyond T
+      float mx = -INFINITY;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          float v = sacc[b][r] * LOG2E;
+          v = key < T ? v : -INFINITY;
+          sacc[b][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float alpha = exp2f(m - mnew);
+      float ps = 0.0f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = exp2f(sacc[b][r] - mnew);
+          sacc[b][r] = pv;
+          ps += pv;
+        }
+      l = l * alpha + ps;
+      m = mnew;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-        sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[b], 0, 0, 0);
-      }
-    }
-    // scores -> log2 domain, mask keys beyond T
-    float mx = -INFINITY;
+        const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        float v = sacc[b][r] * LOG2E;
-        v = key < T ? v : -INFINITY;
-        sacc[b][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(m, mx);
-    const float alpha = exp2f(m - mnew);
-    float ps = 0.0f;
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = exp2f(sacc[b][r] - mnew);
-        sacc[b][r] = pv;
-        ps += pv;
-      }
-    l = l * alpha + ps;
-    m = mnew;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
-#pragma unroll
-      for (int db = 0; db < 2; ++db) {
-        const bf16x8 vf = trans_frag(vt_s, VSTR, 16 * s, 32 * db, lane);
-        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
+        for (int db = 0; db < 2; ++db) {
+          const bf16x8 vf = trans_frag(vt_s, VSTR, 16 * s, 32 * db, lane);
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
+        }
       }
     }
     if (more) {
-      stage_store(ks[cur ^ 1], KSTR, rk, 1.0f);
-      stage_store(vs[cur ^ 1], VSTR, rv, 1.0f);
+      stage_store(ks + (cur ^ 1) * 64 * KSTR, KSTR, rk, 1.0f, lt);
+      stage_store(vs + (cur ^ 1) * 64 * VSTR, VSTR, rv, 1.0f, lt);
     }
     __syncthreads();
   }
-  const float lt = l + __shfl_xor(l, 32, 64);
-  const float inv = 1.0f / lt;
+  if constexpr (KS > 1) {
+    // merge the key-split partials: parts 1.. publish (m, l, O) per lane, part 0 folds them in order
+    float* red = reinterpret_cast<float*>(smem);
+    if (part > 0) {
+      float* dst = red + ((part - 1) * 4 + wid) * 34 * 64 + lane;
+      dst[0] = m;
+      dst[64] = l;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(2 + 16 * db + r) * 64] = oacc[db][r];
+    }
+    __syncthreads();
+    if (part > 0) return;
+#pragma unroll
+    for (int p = 1; p < KS; ++p) {
+      const float* src = red + ((p - 1) * 4 + wid) * 34 * 64 + lane;
+      const float mp = src[0], lp = src[64];
+      const float mn = fmaxf(m, mp);
+      const float a0 = exp2f(m - mn), a1 = exp2f(mp - mn);
+      l = l * a0 + lp * a1;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[db][r] = oacc[db][r] * a0 + src[(2 + 16 * db + r) * 64] * a1;
+      m = mn;
+    }
+  }
+  const float lsum = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.0f / lsum;
   if (qok) {
     bf16* orow = o + ((long)n * T + my_q) * ldo + h * 64;
 #pragma unroll
@@ -192,7 +241,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* qkv, int ld, 
         for (int e = 0; e < 4; ++e) v[e] = (bf16)(oacc[db][4 * g2 + e] * inv);
         *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * g2 + 4 * hh) = v;
       }
-    if (hh == 0) lse[((long)n * heads + h) * T + my_q] = m * LN2 + logf(lt);
+    if (hh == 0) lse[((long)n * heads + h) * T + my_q] = m * LN2 + logf(lsum);
   }
 }
 
@@ -218,13 +267,28 @@ __global__ void attn_delta_kernel(const bf16* o, int ldo, const bf16* dout, int 
   delta[(n * heads + h) * T + q] = s;
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
-                                                            const float* lse, const float* delta, int T, int heads,
-                                                            bf16* dqkv, int ldd) {
-  __shared__ __attribute__((aligned(16))) bf16 qs[2][64 * KSTR];
-  __shared__ __attribute__((aligned(16))) bf16 ds_[2][64 * KSTR];
-  __shared__ float ls[2][64], dl[2][64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+// dK/dV: 128 keys per block resident in registers (32 per wave); KS query-splits per block (waves
+// 4p..4p+3 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a fixed order.
+template <int KS>
+struct DkdvLds {
+  static constexpr int TILE = 64 * KSTR * 2;
+  static constexpr int MAIN = KS * 2 * 2 * TILE + KS * 2 * 2 * 64 * 4;
+  static constexpr int RED = (KS - 1) * 4 * 64 * 64 * 4;
+  static constexpr int BYTES = MAIN > RED ? MAIN : RED;
+};
+
+template <int KS>
+__global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
+                                                                 const float* lse, const float* delta, int T,
+                                                                 int heads, bf16* dqkv, int ldd) {
+  __shared__ __attribute__((aligned(16))) char smem[DkdvLds<KS>::BYTES];
+  const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) & 3, part = threadIdx.x >> 8, hh = lane >> 5;
+  const int lt = threadIdx.x & 255;
+  constexpr int TILE = DkdvLds<KS>::TILE;
+  bf16* qs = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE);       // [2 stages][64 * KSTR]
+  bf16* ds_ = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE + 2 * TILE);
+  float* ls = reinterpret_cast<float*>(smem + KS * 2 * 2 * TILE) + part * 2 * 2 * 64;  // [2][64]
+  float* dl = ls + 2 * 64;
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
@@ -246,72 +310,108 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* qkv, int
     for (int r = 0; r < 16; ++r) { dv[db][r] = 0.0f; dk[db][r] = 0.0f; }
 
   const int ntiles = (T + 63) / 64;
+  const int per = (ntiles + KS - 1) / KS;
+  const int tb = part * per;
+  const int mine = max(0, min(ntiles, tb + per) - tb);
   uint4 rq[2], rd[2];
   float rl = 0.0f, rdl = 0.0f;
   auto load_tile = [&](int qt) {
-    stage_load(base, ld, qt * 64, T, h * 64, rq);
-    stage_load(dob, lddo, qt * 64, T, h * 64, rd);
-    if (threadIdx.x < 64) {
-      const int q = qt * 64 + threadIdx.x;
+    stage_load(base, ld, qt * 64, T, h * 64, rq, lt);
+    stage_load(dob, lddo, qt * 64, T, h * 64, rd, lt);
+    if (lt < 64) {
+      const int q = qt * 64 + lt;
       rl = q < T ? lse_b[q] : INFINITY;
       rdl = q < T ? del_b[q] : 0.0f;
     }
   };
   auto store_tile = [&](int st) {
-    stage_store(qs[st], KSTR, rq, 0.125f);
-    stage_store(ds_[st], KSTR, rd, 1.0f);
-    if (threadIdx.x < 64) {
-      ls[st][threadIdx.x] = rl;
-      dl[st][threadIdx.x] = rdl;
+    stage_store(qs + st * 64 * KSTR, KSTR, rq, 0.125f, lt);
+    stage_store(ds_ + st * 64 * KSTR, KSTR, rd, 1.0f, lt);
+    if (lt < 64) {
+      ls[st * 64 + lt] = rl;
+      dl[st * 64 + lt] = rdl;
     }
   };
-  load_tile(0);
-  store_tile(0);
+  if (mine > 0) {
+    load_tile(tb);
+    store_tile(0);
+  }
   __syncthreads();
-  for (int qt = 0; qt < ntiles; ++qt) {
-    const int cur = qt & 1;
-    const bool more = qt + 1 < ntiles;
+  for (int i = 0; i < per; ++i) {
+    const int qt = tb + i;
+    const int cur = i & 1;
+    const bool more = i + 1 < mine;
     if (more) load_tile(qt + 1);
-    const bf16* qt_s = qs[cur];
-    const bf16* dt_s = ds_[cur];
+    if (i < mine) {
+      const bf16* qt_s = qs + cur * 64 * KSTR;
+      const bf16* dt_s = ds_ + cur * 64 * KSTR;
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      f32x16 sp, dp;
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x16 sp, dp;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qr = 32 * qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        sp[r] = -ls[cur][qr];
-        dp[r] = -dl[cur][qr];
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int qr = 32 * qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          sp[r] = -ls[cur * 64 + qr];
+          dp[r] = -dl[cur * 64 + qr];
+        }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(qt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-        sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sp, 0, 0, 0);
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(dt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
-      }
-      // sp = S - lse -> P ; dp = dP - delta -> dS = P * dp
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 qa =
+              *reinterpret_cast<const bf16x8*>(qt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sp, 0, 0, 0);
+          const bf16x8 da =
+              *reinterpret_cast<const bf16x8*>(dt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
+        }
+        // sp = S - lse -> P ; dp = dP - delta -> dS = P * dp
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = exp2f(sp[r] * LOG2E);
-        sp[r] = pv;
-        dp[r] = pv * dp[r];
-      }
+        for (int r = 0; r < 16; ++r) {
+          const float pv = exp2f(sp[r] * LOG2E);
+          sp[r] = pv;
+          dp[r] = pv * dp[r];
+        }
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 pf = acc_to_frag(sp, s2);
-        const bf16x8 sf = acc_to_frag(dp, s2);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pf = acc_to_frag(sp, s2);
+          const bf16x8 sf = acc_to_frag(dp, s2);
 #pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const bf16x8 doT = trans_frag(dt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
-          dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doT, pf, dv[db], 0, 0, 0);
-          const bf16x8 qT = trans_frag(qt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
-          dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, sf, dk[db], 0, 0, 0);
+          for (int db = 0; db < 2; ++db) {
+            const bf16x8 doT = trans_frag(dt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
+            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doT, pf, dv[db], 0, 0, 0);
+            const bf16x8 qT = trans_frag(qt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
+            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, sf, dk[db], 0, 0, 0);
+          }
         }
       }
     }
     if (more) store_tile(cur ^ 1);
     __syncthreads();
+  }
+  if constexpr (KS > 1) {
+    float* red = reinterpret_cast<float*>(smem);
+    if (part > 0) {
+      float* dst = red + ((part - 1) * 4 + wid) * 64 * 64 + lane;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          dst[(16 * db + r) * 64] = dk[db][r];
+          dst[(32 + 16 * db + r) * 64] = dv[db][r];
+        }
+    }
+    __syncthreads();
+    if (part > 0) return;
+#pragma unroll
+    for (int p = 1; p < KS; ++p) {
+      const float* src = red + ((p - 1) * 4 + wid) * 64 * 64 + lane;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          dk[db][r] += src[(16 * db + r) * 64];
+          dv[db][r] += src[(32 + 16 * db + r) * 64];
+        }
+    }
   }
   if (kok) {
     bf16* row = dqkv + ((long)n * T + my_k) * ldd;
@@ -332,12 +432,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* qkv, int
   }
 }
 
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
-                                                          const float* lse, const float* delta, int T, int heads,
-                                                          bf16* dqkv, int ldd) {
-  __shared__ __attribute__((aligned(16))) bf16 ks[2][64 * KSTR];
-  __shared__ __attribute__((aligned(16))) bf16 vs[2][64 * KSTR];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, hh = lane >> 5;
+// dQ: 128 queries per block resident; KS key-splits per block, partial dQ folded through LDS.
+template <int KS>
+struct DqLds {
+  static constexpr int TILE = 64 * KSTR * 2;
+  static constexpr int MAIN = KS * 2 * 2 * TILE;
+  static constexpr int RED = (KS - 1) * 4 * 32 * 64 * 4;
+  static constexpr int BYTES = MAIN > RED ? MAIN : RED;
+};
+
+template <int KS>
+__global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
+                                                               const float* lse, const float* delta, int T, int heads,
+                                                               bf16* dqkv, int ldd) {
+  __shared__ __attribute__((aligned(16))) char smem[DqLds<KS>::BYTES];
+  const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) & 3, part = threadIdx.x >> 8, hh = lane >> 5;
+  const int lt = threadIdx.x & 255;
+  constexpr int TILE = DqLds<KS>::TILE;
+  bf16* ks = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE);
+  bf16* vs = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE + 2 * TILE);
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
@@ -357,54 +470,82 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* qkv, int l
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[db][r] = 0.0f;
   const int ntiles = (T + 63) / 64;
+  const int per = (ntiles + KS - 1) / KS;
+  const int tb = part * per;
+  const int mine = max(0, min(ntiles, tb + per) - tb);
   uint4 rk[2], rv[2];
-  stage_load(base, ld, 0, T, C + h * 64, rk);
-  stage_load(base, ld, 0, T, 2 * C + h * 64, rv);
-  stage_store(ks[0], KSTR, rk, 1.0f);
-  stage_store(vs[0], KSTR, rv, 1.0f);
+  if (mine > 0) {
+    stage_load(base, ld, tb * 64, T, C + h * 64, rk, lt);
+    stage_load(base, ld, tb * 64, T, 2 * C + h * 64, rv, lt);
+    stage_store(ks, KSTR, rk, 1.0f, lt);
+    stage_store(vs, KSTR, rv, 1.0f, lt);
+  }
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < ntiles;
+  for (int i = 0; i < per; ++i) {
+    const int kt = tb + i;
+    const int cur = i & 1;
+    const bool more = i + 1 < mine;
     if (more) {
-      stage_load(base, ld, (kt + 1) * 64, T, C + h * 64, rk);
-      stage_load(base, ld, (kt + 1) * 64, T, 2 * C + h * 64, rv);
+      stage_load(base, ld, (kt + 1) * 64, T, C + h * 64, rk, lt);
+      stage_load(base, ld, (kt + 1) * 64, T, 2 * C + h * 64, rv, lt);
     }
-    const bf16* kt_s = ks[cur];
-    const bf16* vt_s = vs[cur];
+    if (i < mine) {
+      const bf16* kt_s = ks + cur * 64 * KSTR;
+      const bf16* vt_s = vs + cur * 64 * KSTR;
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      f32x16 sp, dp;
+      for (int b = 0; b < 2; ++b) {
+        f32x16 sp, dp;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sp[r] = 0.0f; dp[r] = 0.0f; }
+        for (int r = 0; r < 16; ++r) { sp[r] = 0.0f; dp[r] = 0.0f; }
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-        sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sp, 0, 0, 0);
-        const bf16x8 va = *reinterpret_cast<const bf16x8*>(vt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dp, 0, 0, 0);
-      }
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sp, 0, 0, 0);
+          const bf16x8 va = *reinterpret_cast<const bf16x8*>(vt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dp, 0, 0, 0);
+        }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float pv = key < T ? exp2f(sp[r] * LOG2E - my_lse) : 0.0f;
-        sp[r] = pv * (dp[r] - my_del);  // dS^T
-      }
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const float pv = key < T ? exp2f(sp[r] * LOG2E - my_lse) : 0.0f;
+          sp[r] = pv * (dp[r] - my_del);  // dS^T
+        }
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 sf = acc_to_frag(sp, s2);
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 sf = acc_to_frag(sp, s2);
 #pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const bf16x8 kT = trans_frag(kt_s, KSTR, 32 * b + 16 * s2, 32 * db, lane);
-          dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kT, sf, dq[db], 0, 0, 0);
+          for (int db = 0; db < 2; ++db) {
+            const bf16x8 kT = trans_frag(kt_s, KSTR, 32 * b + 16 * s2, 32 * db, lane);
+            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kT, sf, dq[db], 0, 0, 0);
+          }
         }
       }
     }
     if (more) {
-      stage_store(ks[cur ^ 1], KSTR, rk, 1.0f);
-      stage_store(vs[cur ^ 1], KSTR, rv, 1.0f);
+      stage_store(ks + (cur ^ 1) * 64 * KSTR, KSTR, rk, 1.0f, lt);
+      stage_store(vs + (cur ^ 1) * 64 * KSTR, KSTR, rv, 1.0f, lt);
     }
     __syncthreads();
+  }
+  if constexpr (KS > 1) {
+    float* red = reinterpret_cast<float*>(smem);
+    if (part > 0) {
+      float* dst = red + ((part - 1) * 4 + wid) * 32 * 64 + lane;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(16 * db + r) * 64] = dq[db][r];
+    }
+    __syncthreads();
+    if (part > 0) return;
+#pragma unroll
+    for (int p = 1; p < KS; ++p) {
+      const float* src = red + ((p - 1) * 4 + wid) * 32 * 64 + lane;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[db][r] += src[(16 * db + r) * 64];
+    }
   }
   if (qok) {
     bf16* row = dqkv + ((long)n * T + my_q) * ldd + h * 64;
@@ -578,13 +719,30 @@ __global__ void cross_bwd_kernel(const bf16* x, int ldx, long rows, int c, int h
 
 }  // namespace
 
+namespace {
+// DC_ATTN_KS=1|2 overrides the automatic choice (benchmarks / tests)
+int attn_ks(dim3 grid) {
+  static int forced = [] {
+    const char* e = getenv("DC_ATTN_KS");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 1 || forced == 2) return forced;
+  return (long)grid.x * grid.y * grid.z < 1024 ? 2 : 1;
+}
+}  // namespace
+
 extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse,
                            void* stream) {
   if (!qkv || !o || !lse || nb <= 0 || t <= 0 || heads <= 0) return DC_ERR_ARG;
   if (ld % 8 || ldo % 8 || ld < 3 * heads * 64 || ldo < heads * 64) return DC_ERR_ALIGN;
   dim3 grid((t + 127) / 128, heads, nb);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ld, t, heads,
-                     (bf16*)o, ldo, lse);
+  // key-split factor: enough resident waves per CU when (query blocks x heads x frames) is small
+  if (attn_ks(grid) == 2)
+    hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(512), 0, (hipStream_t)stream, (const bf16*)qkv, ld, t, heads,
+                       (bf16*)o, ldo, lse);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ld, t, heads,
+                       (bf16*)o, ldo, lse);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -599,10 +757,17 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)o, ldo,
                      (const bf16*)dout, lddo, t, heads, total, delta_ws);
   dim3 grid((t + 127) / 128, heads, nb);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid, dim3(256), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo, lse,
-                     delta_ws, t, heads, (bf16*)dqkv, ldd);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo, lse,
-                     delta_ws, t, heads, (bf16*)dqkv, ldd);
+  if (attn_ks(grid) == 2) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, grid, dim3(512), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
+                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, grid, dim3(512), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
+                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, grid, dim3(256), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
+                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, grid, dim3(256), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
+                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
+  }
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

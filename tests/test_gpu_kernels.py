@@ -199,7 +199,8 @@ def test_layernorm_fwd_bwd(ctx, c):
 
 
 # ----------------------------------------------------------------------------- attention
-@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (2, 300, 2), (1, 1000, 5), (1, 108, 20)])
+# the last shape launches >= 1024 blocks (no key split), the others the 2-way key-split kernels
+@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (2, 300, 2), (1, 1000, 5), (1, 108, 20), (16, 1000, 8)])
 def test_attention_fwd_bwd(ctx, n, t, heads):
     from depth_completion_amd import ops
     C = heads * 64
