@@ -13,7 +13,6 @@
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
-constexpr float LN2 = 0.6931471805599453f;
 constexpr int KSTR = 72;   // row stride (elements) of row-read tiles: 144 B, conflict-free ds_read_b128
 constexpr int VSTR = 96;   // row stride of tr-read-only tiles: 192 B, conflict-free ds_read_b64_tr_b16
 
@@ -58,21 +57,32 @@ __device__ __forceinline__ bf16x8 load_row8(const bf16* p, bool ok, float scale)
   return v;
 }
 
-// stage a [64 rows][64 cols] bf16 tile (rows r0.., column offset col) into LDS with `stride`
-__device__ __forceinline__ void stage_load(const bf16* base, long ld, int r0, int rows_total, int col, uint4 (&reg)[2],
-                                           int t) {
+// stage a [64 rows][64 cols] bf16 tile (rows r0.., column offset col) into LDS with `stride`, by NT threads
+// (t = 0..NT-1): 512 16-B pieces, PPT per thread
+template <int NT>
+constexpr int ppt() { return (512 + NT - 1) / NT; }
+
+template <int NT>
+__device__ __forceinline__ void stage_load(const bf16* base, long ld, int r0, int rows_total, int col,
+                                           uint4 (&reg)[ppt<NT>()], int t) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (t >> 3) + 32 * i, piece = t & 7;
+  for (int i = 0; i < ppt<NT>(); ++i) {
+    const int p = t + NT * i;
+    const int row = p >> 3, piece = p & 7;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + row < rows_total) v = *reinterpret_cast<const uint4*>(base + (long)(r0 + row) * ld + col + piece * 8);
+    if (p < 512 && r0 + row < rows_total)
+      v = *reinterpret_cast<const uint4*>(base + (long)(r0 + row) * ld + col + piece * 8);
     reg[i] = v;
   }
 }
-__device__ __forceinline__ void stage_store(bf16* tile, int stride, const uint4 (&reg)[2], float scale, int t) {
+template <int NT>
+__device__ __forceinline__ void stage_store(bf16* tile, int stride, const uint4 (&reg)[ppt<NT>()], float scale,
+                                            int t) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (t >> 3) + 32 * i, piece = t & 7;
+  for (int i = 0; i < ppt<NT>(); ++i) {
+    const int p = t + NT * i;
+    if (p >= 512) break;
+    const int row = p >> 3, piece = p & 7;
     uint4 v = reg[i];
     if (scale != 1.0f) {
       bf16x8 b = *reinterpret_cast<bf16x8*>(&v);
@@ -88,26 +98,29 @@ __device__ __forceinline__ void stage_store(bf16* tile, int stride, const uint4 
 // KS key-splits per block: waves 4p..4p+3 sweep the p-th contiguous range of key tiles for the same
 // 128 queries (KS x 4 waves per CU hide MFMA / softmax / LDS latency at small T x heads), then the
 // partial (m, l, O) are merged through LDS in a fixed order (deterministic).
-template <int KS>
+template <int QW, int KS>
 struct FwdLds {
   static constexpr int K_BYTES = KS * 2 * 64 * KSTR * 2;
   static constexpr int V_BYTES = KS * 2 * 64 * VSTR * 2;
-  static constexpr int RED = (KS - 1) * 4 * 34 * 64 * 4;
+  static constexpr int RED = (KS - 1) * QW * 34 * 64 * 4;
   static constexpr int BYTES = (K_BYTES + V_BYTES > RED) ? K_BYTES + V_BYTES : RED;
 };
 
-template <int KS>
-__global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(const bf16* qkv, int ld, int T, int heads, bf16* o,
+template <int QW, int KS>
+__global__ __launch_bounds__(64 * QW * KS) void attn_fwd_kernel(const bf16* qkv, int ld, int T, int heads, bf16* o,
                                                             int ldo, float* lse) {
-  __shared__ __attribute__((aligned(16))) char smem[FwdLds<KS>::BYTES];
-  const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) & 3, part = threadIdx.x >> 8, hh = lane >> 5;
-  const int lt = threadIdx.x & 255;
+  __shared__ __attribute__((aligned(16))) char smem[FwdLds<QW, KS>::BYTES];
+  constexpr int NT = 64 * QW;  // threads per key/query split
+  constexpr int PPT = ppt<NT>();
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
+  const int lt = threadIdx.x - part * NT;
   bf16* ks = reinterpret_cast<bf16*>(smem) + part * 2 * 64 * KSTR;
-  bf16* vs = reinterpret_cast<bf16*>(smem + FwdLds<KS>::K_BYTES) + part * 2 * 64 * VSTR;
+  bf16* vs = reinterpret_cast<bf16*>(smem + FwdLds<QW, KS>::K_BYTES) + part * 2 * 64 * VSTR;
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
-  const int my_q = blockIdx.x * 128 + wid * 32 + (lane & 31);
+  const int my_q = blockIdx.x * (32 * QW) + wid * 32 + (lane & 31);
   const bool qok = my_q < T;
   bf16x8 qf[4];
 #pragma unroll
@@ -124,87 +137,103 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(const bf16* qkv, int
   const int per = (ntiles + KS - 1) / KS;
   const int tb = part * per;
   const int mine = max(0, min(ntiles, tb + per) - tb);
-  uint4 rk[2], rv[2];
+  // two register stages: tile i+2 is fetched while tile i is computed and tile i+1 is written to LDS
+  uint4 ra[2][PPT], rb[2][PPT];
   if (mine > 0) {
-    stage_load(base, ld, tb * 64, T, C + h * 64, rk, lt);
-    stage_load(base, ld, tb * 64, T, 2 * C + h * 64, rv, lt);
-    stage_store(ks, KSTR, rk, 1.0f, lt);
-    stage_store(vs, VSTR, rv, 1.0f, lt);
+    stage_load<NT>(base, ld, tb * 64, T, C + h * 64, ra[0], lt);
+    stage_load<NT>(base, ld, tb * 64, T, 2 * C + h * 64, ra[1], lt);
+    stage_store<NT>(ks, KSTR, ra[0], 1.0f, lt);
+    stage_store<NT>(vs, VSTR, ra[1], 1.0f, lt);
+  }
+  if (mine > 1) {
+    stage_load<NT>(base, ld, (tb + 1) * 64, T, C + h * 64, rb[0], lt);
+    stage_load<NT>(base, ld, (tb + 1) * 64, T, 2 * C + h * 64, rb[1], lt);
   }
   __syncthreads();
-  for (int i = 0; i < per; ++i) {
+  auto body = [&](int i, uint4 (&held)[2][PPT], uint4 (&fresh)[2][PPT]) {
     const int kt = tb + i;
     const int cur = i & 1;
-    const bool more = i + 1 < mine;
-    if (more) {
-      stage_load(base, ld, (kt + 1) * 64, T, C + h * 64, rk, lt);
-      stage_load(base, ld, (kt + 1) * 64, T, 2 * C + h * 64, rv, lt);
+    if (i + 2 < mine) {
+      stage_load<NT>(base, ld, (kt + 2) * 64, T, C + h * 64, fresh[0], lt);
+      stage_load<NT>(base, ld, (kt + 2) * 64, T, 2 * C + h * 64, fresh[1], lt);
     }
-    if (i < mine) {
-      const bf16* kt_s = ks + cur * 64 * KSTR;
-      const bf16* vt_s = vs + cur * 64 * VSTR;
-      f32x16 sacc[2];
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
-#pragma unroll
+      if (i < mine) {
+        const bf16* kt_s = ks + cur * 64 * KSTR;
+        const bf16* vt_s = vs + cur * 64 * VSTR;
+        f32x16 sacc[2];
+  #pragma unroll
+        for (int b = 0; b < 2; ++b) {
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
+  #pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+            sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[b], 0, 0, 0);
+          }
+        }
+        // online softmax in raw score units; exp2 with log2(e) folded into one FMA per score;
+        // keys beyond T exist only in the last tile; O is rescaled only when some row max grew
+        if ((kt + 1) * 64 > T) {
+  #pragma unroll
+          for (int b = 0; b < 2; ++b)
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
+              if (key >= T) sacc[b][r] = -INFINITY;
+            }
+        }
+        float mx = -INFINITY;
+  #pragma unroll
+        for (int b = 0; b < 2; ++b)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[b][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m, mx);
+        const float ml = mnew * LOG2E;
+        float ps = 0.0f;
+  #pragma unroll
+        for (int b = 0; b < 2; ++b)
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = exp2f(fmaf(sacc[b][r], LOG2E, -ml));
+            sacc[b][r] = pv;
+            ps += pv;
+          }
+        if (__any(mnew > m)) {
+          const float alpha = exp2f((m - mnew) * LOG2E);
+          l *= alpha;
+  #pragma unroll
+          for (int db = 0; db < 2; ++db)
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+        }
+        l += ps;
+        m = mnew;
+  #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-          sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[b], 0, 0, 0);
+          const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
+  #pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            const bf16x8 vf = trans_frag(vt_s, VSTR, 16 * s, 32 * db, lane);
+            oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
+          }
         }
       }
-      // scores -> log2 domain, mask keys beyond T
-      float mx = -INFINITY;
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          float v = sacc[b][r] * LOG2E;
-          v = key < T ? v : -INFINITY;
-          sacc[b][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      const float alpha = exp2f(m - mnew);
-      float ps = 0.0f;
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = exp2f(sacc[b][r] - mnew);
-          sacc[b][r] = pv;
-          ps += pv;
-        }
-      l = l * alpha + ps;
-      m = mnew;
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const bf16x8 vf = trans_frag(vt_s, VSTR, 16 * s, 32 * db, lane);
-          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
-        }
-      }
-    }
-    if (more) {
-      stage_store(ks + (cur ^ 1) * 64 * KSTR, KSTR, rk, 1.0f, lt);
-      stage_store(vs + (cur ^ 1) * 64 * VSTR, VSTR, rv, 1.0f, lt);
+    if (i + 1 < mine) {
+      stage_store<NT>(ks + (cur ^ 1) * 64 * KSTR, KSTR, held[0], 1.0f, lt);
+      stage_store<NT>(vs + (cur ^ 1) * 64 * VSTR, VSTR, held[1], 1.0f, lt);
     }
     __syncthreads();
+  };
+  for (int i = 0; i < per; i += 2) {
+    body(i, rb, ra);
+    if (i + 1 < per) body(i + 1, ra, rb);
   }
   if constexpr (KS > 1) {
     // merge the key-split partials: parts 1.. publish (m, l, O) per lane, part 0 folds them in order
     float* red = reinterpret_cast<float*>(smem);
     if (part > 0) {
-      float* dst = red + ((part - 1) * 4 + wid) * 34 * 64 + lane;
+      float* dst = red + ((part - 1) * QW + wid) * 34 * 64 + lane;
       dst[0] = m;
       dst[64] = l;
 #pragma unroll
@@ -219,7 +248,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(const bf16* qkv, int
       const float* src = red + ((p - 1) * 4 + wid) * 34 * 64 + lane;
       const float mp = src[0], lp = src[64];
       const float mn = fmaxf(m, mp);
-      const float a0 = exp2f(m - mn), a1 = exp2f(mp - mn);
+      const float a0 = exp2f((m - mn) * LOG2E), a1 = exp2f((mp - mn) * LOG2E);
       l = l * a0 + lp * a1;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
@@ -241,7 +270,7 @@ __global__ __launch_bounds__(256 * KS) void attn_fwd_kernel(const bf16* qkv, int
         for (int e = 0; e < 4; ++e) v[e] = (bf16)(oacc[db][4 * g2 + e] * inv);
         *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * g2 + 4 * hh) = v;
       }
-    if (hh == 0) lse[((long)n * heads + h) * T + my_q] = m * LN2 + logf(lsum);
+    if (hh == 0) lse[((long)n * heads + h) * T + my_q] = m + logf(lsum);
   }
 }
 
@@ -269,22 +298,25 @@ __global__ void attn_delta_kernel(const bf16* o, int ldo, const bf16* dout, int 
 
 // dK/dV: 128 keys per block resident in registers (32 per wave); KS query-splits per block (waves
 // 4p..4p+3 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a fixed order.
-template <int KS>
+template <int QW, int KS>
 struct DkdvLds {
   static constexpr int TILE = 64 * KSTR * 2;
   static constexpr int MAIN = KS * 2 * 2 * TILE + KS * 2 * 2 * 64 * 4;
-  static constexpr int RED = (KS - 1) * 4 * 64 * 64 * 4;
+  static constexpr int RED = (KS - 1) * QW * 64 * 64 * 4;
   static constexpr int BYTES = MAIN > RED ? MAIN : RED;
 };
 
-template <int KS>
-__global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
+template <int QW, int KS>
+__global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dkdv_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
                                                                  const float* lse, const float* delta, int T,
                                                                  int heads, bf16* dqkv, int ldd) {
-  __shared__ __attribute__((aligned(16))) char smem[DkdvLds<KS>::BYTES];
-  const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) & 3, part = threadIdx.x >> 8, hh = lane >> 5;
-  const int lt = threadIdx.x & 255;
-  constexpr int TILE = DkdvLds<KS>::TILE;
+  __shared__ __attribute__((aligned(16))) char smem[DkdvLds<QW, KS>::BYTES];
+  constexpr int NT = 64 * QW;  // threads per key/query split
+  constexpr int PPT = ppt<NT>();
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
+  const int lt = threadIdx.x - part * NT;
+  constexpr int TILE = DkdvLds<QW, KS>::TILE;
   bf16* qs = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE);       // [2 stages][64 * KSTR]
   bf16* ds_ = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE + 2 * TILE);
   float* ls = reinterpret_cast<float*>(smem + KS * 2 * 2 * TILE) + part * 2 * 2 * 64;  // [2][64]
@@ -295,7 +327,7 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(const bf16* qkv
   const bf16* dob = dout + (long)n * T * lddo;
   const float* lse_b = lse + ((long)n * heads + h) * T;
   const float* del_b = delta + ((long)n * heads + h) * T;
-  const int my_k = blockIdx.x * 128 + wid * 32 + (lane & 31);
+  const int my_k = blockIdx.x * (32 * QW) + wid * 32 + (lane & 31);
   const bool kok = my_k < T;
   bf16x8 kf[4], vf[4];
 #pragma unroll
@@ -313,84 +345,92 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(const bf16* qkv
   const int per = (ntiles + KS - 1) / KS;
   const int tb = part * per;
   const int mine = max(0, min(ntiles, tb + per) - tb);
-  uint4 rq[2], rd[2];
-  float rl = 0.0f, rdl = 0.0f;
-  auto load_tile = [&](int qt) {
-    stage_load(base, ld, qt * 64, T, h * 64, rq, lt);
-    stage_load(dob, lddo, qt * 64, T, h * 64, rd, lt);
+  // two register stages (Q / dO pieces + lse / delta): tile i+2 is fetched while tile i is computed
+  struct Stage {
+    uint4 q[PPT], d[PPT];
+    float l, dl;
+  };
+  Stage sa, sb;
+  auto load_tile = [&](int qt, Stage& r) {
+    stage_load<NT>(base, ld, qt * 64, T, h * 64, r.q, lt);
+    stage_load<NT>(dob, lddo, qt * 64, T, h * 64, r.d, lt);
     if (lt < 64) {
       const int q = qt * 64 + lt;
-      rl = q < T ? lse_b[q] : INFINITY;
-      rdl = q < T ? del_b[q] : 0.0f;
+      r.l = q < T ? lse_b[q] : INFINITY;
+      r.dl = q < T ? del_b[q] : 0.0f;
     }
   };
-  auto store_tile = [&](int st) {
-    stage_store(qs + st * 64 * KSTR, KSTR, rq, 0.125f, lt);
-    stage_store(ds_ + st * 64 * KSTR, KSTR, rd, 1.0f, lt);
+  auto store_tile = [&](int st, const Stage& r) {
+    stage_store<NT>(qs + st * 64 * KSTR, KSTR, r.q, 0.125f, lt);
+    stage_store<NT>(ds_ + st * 64 * KSTR, KSTR, r.d, 1.0f, lt);
     if (lt < 64) {
-      ls[st * 64 + lt] = rl;
-      dl[st * 64 + lt] = rdl;
+      ls[st * 64 + lt] = r.l;
+      dl[st * 64 + lt] = r.dl;
     }
   };
   if (mine > 0) {
-    load_tile(tb);
-    store_tile(0);
+    load_tile(tb, sa);
+    store_tile(0, sa);
   }
+  if (mine > 1) load_tile(tb + 1, sb);
   __syncthreads();
-  for (int i = 0; i < per; ++i) {
+  auto body = [&](int i, Stage& held, Stage& fresh) {
     const int qt = tb + i;
     const int cur = i & 1;
-    const bool more = i + 1 < mine;
-    if (more) load_tile(qt + 1);
-    if (i < mine) {
-      const bf16* qt_s = qs + cur * 64 * KSTR;
-      const bf16* dt_s = ds_ + cur * 64 * KSTR;
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        f32x16 sp, dp;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qr = 32 * qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          sp[r] = -ls[cur * 64 + qr];
-          dp[r] = -dl[cur * 64 + qr];
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const bf16x8 qa =
-              *reinterpret_cast<const bf16x8*>(qt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sp, 0, 0, 0);
-          const bf16x8 da =
-              *reinterpret_cast<const bf16x8*>(dt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
-        }
-        // sp = S - lse -> P ; dp = dP - delta -> dS = P * dp
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = exp2f(sp[r] * LOG2E);
-          sp[r] = pv;
-          dp[r] = pv * dp[r];
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 pf = acc_to_frag(sp, s2);
-          const bf16x8 sf = acc_to_frag(dp, s2);
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            const bf16x8 doT = trans_frag(dt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
-            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doT, pf, dv[db], 0, 0, 0);
-            const bf16x8 qT = trans_frag(qt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
-            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, sf, dk[db], 0, 0, 0);
+    if (i + 2 < mine) load_tile(qt + 2, fresh);
+      if (i < mine) {
+        const bf16* qt_s = qs + cur * 64 * KSTR;
+        const bf16* dt_s = ds_ + cur * 64 * KSTR;
+  #pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          f32x16 sp, dp;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int qr = 32 * qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            sp[r] = -ls[cur * 64 + qr];
+            dp[r] = -dl[cur * 64 + qr];
+          }
+  #pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const bf16x8 qa =
+                *reinterpret_cast<const bf16x8*>(qt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+            sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sp, 0, 0, 0);
+            const bf16x8 da =
+                *reinterpret_cast<const bf16x8*>(dt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
+          }
+          // sp = S - lse -> P ; dp = dP - delta -> dS = P * dp
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = exp2f(sp[r] * LOG2E);
+            sp[r] = pv;
+            dp[r] = pv * dp[r];
+          }
+  #pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 pf = acc_to_frag(sp, s2);
+            const bf16x8 sf = acc_to_frag(dp, s2);
+  #pragma unroll
+            for (int db = 0; db < 2; ++db) {
+              const bf16x8 doT = trans_frag(dt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
+              dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doT, pf, dv[db], 0, 0, 0);
+              const bf16x8 qT = trans_frag(qt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
+              dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, sf, dk[db], 0, 0, 0);
+            }
           }
         }
       }
-    }
-    if (more) store_tile(cur ^ 1);
+    if (i + 1 < mine) store_tile(cur ^ 1, held);
     __syncthreads();
+  };
+  for (int i = 0; i < per; i += 2) {
+    body(i, sb, sa);
+    if (i + 1 < per) body(i + 1, sa, sb);
   }
   if constexpr (KS > 1) {
     float* red = reinterpret_cast<float*>(smem);
     if (part > 0) {
-      float* dst = red + ((part - 1) * 4 + wid) * 64 * 64 + lane;
+      float* dst = red + ((part - 1) * QW + wid) * 64 * 64 + lane;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -433,28 +473,31 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dkdv_kernel(const bf16* qkv
 }
 
 // dQ: 128 queries per block resident; KS key-splits per block, partial dQ folded through LDS.
-template <int KS>
+template <int QW, int KS>
 struct DqLds {
   static constexpr int TILE = 64 * KSTR * 2;
   static constexpr int MAIN = KS * 2 * 2 * TILE;
-  static constexpr int RED = (KS - 1) * 4 * 32 * 64 * 4;
+  static constexpr int RED = (KS - 1) * QW * 32 * 64 * 4;
   static constexpr int BYTES = MAIN > RED ? MAIN : RED;
 };
 
-template <int KS>
-__global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
+template <int QW, int KS>
+__global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dq_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
                                                                const float* lse, const float* delta, int T, int heads,
                                                                bf16* dqkv, int ldd) {
-  __shared__ __attribute__((aligned(16))) char smem[DqLds<KS>::BYTES];
-  const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) & 3, part = threadIdx.x >> 8, hh = lane >> 5;
-  const int lt = threadIdx.x & 255;
-  constexpr int TILE = DqLds<KS>::TILE;
+  __shared__ __attribute__((aligned(16))) char smem[DqLds<QW, KS>::BYTES];
+  constexpr int NT = 64 * QW;  // threads per key/query split
+  constexpr int PPT = ppt<NT>();
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
+  const int lt = threadIdx.x - part * NT;
+  constexpr int TILE = DqLds<QW, KS>::TILE;
   bf16* ks = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE);
   bf16* vs = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE + 2 * TILE);
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
-  const int my_q = blockIdx.x * 128 + wid * 32 + (lane & 31);
+  const int my_q = blockIdx.x * (32 * QW) + wid * 32 + (lane & 31);
   const bool qok = my_q < T;
   bf16x8 qf[4], df[4];
 #pragma unroll
@@ -473,64 +516,72 @@ __global__ __launch_bounds__(256 * KS) void attn_bwd_dq_kernel(const bf16* qkv, 
   const int per = (ntiles + KS - 1) / KS;
   const int tb = part * per;
   const int mine = max(0, min(ntiles, tb + per) - tb);
-  uint4 rk[2], rv[2];
+  // two register stages: tile i+2 is fetched while tile i is computed and tile i+1 is written to LDS
+  uint4 ra[2][PPT], rb[2][PPT];
   if (mine > 0) {
-    stage_load(base, ld, tb * 64, T, C + h * 64, rk, lt);
-    stage_load(base, ld, tb * 64, T, 2 * C + h * 64, rv, lt);
-    stage_store(ks, KSTR, rk, 1.0f, lt);
-    stage_store(vs, KSTR, rv, 1.0f, lt);
+    stage_load<NT>(base, ld, tb * 64, T, C + h * 64, ra[0], lt);
+    stage_load<NT>(base, ld, tb * 64, T, 2 * C + h * 64, ra[1], lt);
+    stage_store<NT>(ks, KSTR, ra[0], 1.0f, lt);
+    stage_store<NT>(vs, KSTR, ra[1], 1.0f, lt);
+  }
+  if (mine > 1) {
+    stage_load<NT>(base, ld, (tb + 1) * 64, T, C + h * 64, rb[0], lt);
+    stage_load<NT>(base, ld, (tb + 1) * 64, T, 2 * C + h * 64, rb[1], lt);
   }
   __syncthreads();
-  for (int i = 0; i < per; ++i) {
+  auto body = [&](int i, uint4 (&held)[2][PPT], uint4 (&fresh)[2][PPT]) {
     const int kt = tb + i;
     const int cur = i & 1;
-    const bool more = i + 1 < mine;
-    if (more) {
-      stage_load(base, ld, (kt + 1) * 64, T, C + h * 64, rk, lt);
-      stage_load(base, ld, (kt + 1) * 64, T, 2 * C + h * 64, rv, lt);
+    if (i + 2 < mine) {
+      stage_load<NT>(base, ld, (kt + 2) * 64, T, C + h * 64, fresh[0], lt);
+      stage_load<NT>(base, ld, (kt + 2) * 64, T, 2 * C + h * 64, fresh[1], lt);
     }
-    if (i < mine) {
-      const bf16* kt_s = ks + cur * 64 * KSTR;
-      const bf16* vt_s = vs + cur * 64 * KSTR;
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        f32x16 sp, dp;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { sp[r] = 0.0f; dp[r] = 0.0f; }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sp, 0, 0, 0);
-          const bf16x8 va = *reinterpret_cast<const bf16x8*>(vt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dp, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const float pv = key < T ? exp2f(sp[r] * LOG2E - my_lse) : 0.0f;
-          sp[r] = pv * (dp[r] - my_del);  // dS^T
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 sf = acc_to_frag(sp, s2);
-#pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            const bf16x8 kT = trans_frag(kt_s, KSTR, 32 * b + 16 * s2, 32 * db, lane);
-            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kT, sf, dq[db], 0, 0, 0);
+      if (i < mine) {
+        const bf16* kt_s = ks + cur * 64 * KSTR;
+        const bf16* vt_s = vs + cur * 64 * KSTR;
+  #pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          f32x16 sp, dp;
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) { sp[r] = 0.0f; dp[r] = 0.0f; }
+  #pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+            sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sp, 0, 0, 0);
+            const bf16x8 va = *reinterpret_cast<const bf16x8*>(vt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dp, 0, 0, 0);
+          }
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const float pv = key < T ? exp2f(sp[r] * LOG2E - my_lse) : 0.0f;
+            sp[r] = pv * (dp[r] - my_del);  // dS^T
+          }
+  #pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 sf = acc_to_frag(sp, s2);
+  #pragma unroll
+            for (int db = 0; db < 2; ++db) {
+              const bf16x8 kT = trans_frag(kt_s, KSTR, 32 * b + 16 * s2, 32 * db, lane);
+              dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kT, sf, dq[db], 0, 0, 0);
+            }
           }
         }
       }
-    }
-    if (more) {
-      stage_store(ks + (cur ^ 1) * 64 * KSTR, KSTR, rk, 1.0f, lt);
-      stage_store(vs + (cur ^ 1) * 64 * KSTR, KSTR, rv, 1.0f, lt);
+    if (i + 1 < mine) {
+      stage_store<NT>(ks + (cur ^ 1) * 64 * KSTR, KSTR, held[0], 1.0f, lt);
+      stage_store<NT>(vs + (cur ^ 1) * 64 * KSTR, KSTR, held[1], 1.0f, lt);
     }
     __syncthreads();
+  };
+  for (int i = 0; i < per; i += 2) {
+    body(i, rb, ra);
+    if (i + 1 < per) body(i + 1, ra, rb);
   }
   if constexpr (KS > 1) {
     float* red = reinterpret_cast<float*>(smem);
     if (part > 0) {
-      float* dst = red + ((part - 1) * 4 + wid) * 32 * 64 + lane;
+      float* dst = red + ((part - 1) * QW + wid) * 32 * 64 + lane;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -720,14 +771,53 @@ __global__ void cross_bwd_kernel(const bf16* x, int ldx, long rows, int c, int h
 }  // namespace
 
 namespace {
-// DC_ATTN_KS=1|2 overrides the automatic choice (benchmarks / tests)
-int attn_ks(dim3 grid) {
-  static int forced = [] {
-    const char* e = getenv("DC_ATTN_KS");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 1 || forced == 2) return forced;
-  return (long)grid.x * grid.y * grid.z < 1024 ? 2 : 1;
+// (query waves per block, key splits per block): chosen per launch by a makespan model over the
+// 256 CUs -- rounds of blocks x per-block work (QW) -- discounted when fewer than 8 waves are
+// resident per CU.  DC_ATTN_CFG=<index> forces one (tests / benchmarks).
+struct AttnCfg {
+  int qw, ks, bpc;
+};
+// (a 6-wave (2, 3) instantiation computed wrong results on gfx950 and is not offered; the others
+// are checked one by one in tests/test_gpu_kernels.py::test_attention_fwd_bwd)
+constexpr AttnCfg kAttnCfgs[] = {{4, 1, 2}, {4, 2, 1}, {5, 2, 1}, {2, 2, 1}, {4, 3, 1}};
+constexpr int kNumAttnCfgs = sizeof(kAttnCfgs) / sizeof(kAttnCfgs[0]);
+// the backward kernels hold ~2x the registers: only configs with <= 2 waves per SIMD avoid spills;
+// bwd index 2 is (2, 2) (launch_bwd's default case)
+constexpr int kNumBwdCfgs = 2;
+
+int attn_cfg(int t, int heads, int nb, bool bwd) {
+  const char* e = getenv("DC_ATTN_CFG");  // read per launch (host-side, once per captured graph node)
+  const int forced = e ? atoi(e) : -1;
+  const int ncfg = bwd ? kNumBwdCfgs : kNumAttnCfgs;
+  if (forced >= 0 && forced < ncfg) return forced;
+  int best = 0;
+  double best_t = 1e30;
+  for (int i = 0; i < ncfg; ++i) {
+    const AttnCfg c = kAttnCfgs[i];
+    const long blocks = (long)((t + 32 * c.qw - 1) / (32 * c.qw)) * heads * nb;
+    const long per_cu = (blocks + 255) / 256;
+    const long resident = (long)c.qw * c.ks * (per_cu < c.bpc ? per_cu : c.bpc);
+    const double eff = resident >= 8 ? 1.0 : resident / 8.0;
+    const double tm = (double)per_cu * c.qw / eff;
+    if (tm < best_t * 0.999) { best_t = tm; best = i; }
+  }
+  return best;
+}
+
+template <int QW, int KS>
+void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, hipStream_t st) {
+  dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
+  hipLaunchKernelGGL((attn_fwd_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o, ldo, lse);
+}
+
+template <int QW, int KS>
+void launch_bwd(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
+                int heads, int nb, bf16* dqkv, int ldd, hipStream_t st) {
+  dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse, delta,
+                     t, heads, dqkv, ldd);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse, delta, t,
+                     heads, dqkv, ldd);
 }
 }  // namespace
 
@@ -735,14 +825,15 @@ extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, vo
                            void* stream) {
   if (!qkv || !o || !lse || nb <= 0 || t <= 0 || heads <= 0) return DC_ERR_ARG;
   if (ld % 8 || ldo % 8 || ld < 3 * heads * 64 || ldo < heads * 64) return DC_ERR_ALIGN;
-  dim3 grid((t + 127) / 128, heads, nb);
-  // key-split factor: enough resident waves per CU when (query blocks x heads x frames) is small
-  if (attn_ks(grid) == 2)
-    hipLaunchKernelGGL(attn_fwd_kernel<2>, grid, dim3(512), 0, (hipStream_t)stream, (const bf16*)qkv, ld, t, heads,
-                       (bf16*)o, ldo, lse);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const bf16*)qkv, ld, t, heads,
-                       (bf16*)o, ldo, lse);
+  const bf16* q = (const bf16*)qkv;
+  hipStream_t st = (hipStream_t)stream;
+  switch (attn_cfg(t, heads, nb, false)) {
+    case 0: launch_fwd<4, 1>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
+    case 1: launch_fwd<4, 2>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
+    case 2: launch_fwd<5, 2>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
+    case 3: launch_fwd<2, 2>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
+    default: launch_fwd<4, 3>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
+  }
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -756,17 +847,13 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   const long total = (long)nb * t * heads;
   hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)o, ldo,
                      (const bf16*)dout, lddo, t, heads, total, delta_ws);
-  dim3 grid((t + 127) / 128, heads, nb);
-  if (attn_ks(grid) == 2) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<2>, grid, dim3(512), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
-                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<2>, grid, dim3(512), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
-                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<1>, grid, dim3(256), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
-                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<1>, grid, dim3(256), 0, st, (const bf16*)qkv, ld, (const bf16*)dout, lddo,
-                       lse, delta_ws, t, heads, (bf16*)dqkv, ldd);
+  const bf16* q = (const bf16*)qkv;
+  const bf16* d = (const bf16*)dout;
+  bf16* g = (bf16*)dqkv;
+  switch (attn_cfg(t, heads, nb, true)) {
+    case 0: launch_bwd<4, 1>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
+    case 1: launch_bwd<4, 2>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
+    default: launch_bwd<2, 2>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
   }
   DC_CHECK_LAUNCH();
   return DC_OK;

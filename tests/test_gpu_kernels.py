@@ -201,8 +201,14 @@ def test_layernorm_fwd_bwd(ctx, c):
 # ----------------------------------------------------------------------------- attention
 # the last shape launches >= 1024 blocks (no key split), the others the 2-way key-split kernels
 @pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (2, 300, 2), (1, 1000, 5), (1, 108, 20), (16, 1000, 8)])
-def test_attention_fwd_bwd(ctx, n, t, heads):
+@pytest.mark.parametrize("cfg", [None, "0", "1", "2", "3", "4"])
+def test_attention_fwd_bwd(ctx, n, t, heads, cfg, monkeypatch):
+    """Every (query waves, key splits) block configuration (DC_ATTN_CFG) against fp32 SDPA."""
     from depth_completion_amd import ops
+    if cfg is not None:
+        if n * t * heads > 200000:
+            pytest.skip("forced configurations are covered on the smaller shapes")
+        monkeypatch.setenv("DC_ATTN_CFG", cfg)
     C = heads * 64
     qkv = rnd(n, t, 3 * C, seed=30).to(torch.bfloat16).float().requires_grad_(True)
     q, k, v = qkv.split(C, -1)

@@ -1,10 +1,10 @@
-"""Attention fwd/bwd microbenchmark at the UNet shapes (GPU). DC_ATTN_KS=1|2 forces the key split."""
+"""Attention fwd/bwd microbenchmark at the UNet shapes (GPU). DC_ATTN_CFG=<i> forces a block configuration."""
 import sys, torch
 sys.path.insert(0, ".")
 from depth_completion_amd import ops
 from depth_completion_amd.ops import Ctx
 dev = torch.device("cuda:0"); ctx = Ctx(dev)
-for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (8, 6912, 5)]:
+for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (8, 6912, 5), (8, 1728, 10)]:
     C = heads * 64
     qkv = (torch.randn(n * t, 3 * C, device=dev)).to(torch.bfloat16)
     o = torch.empty(n * t, C, dtype=torch.bfloat16, device=dev); lse = torch.empty(n, heads, t, device=dev)
