@@ -40,14 +40,28 @@ struct ConvGemmParams {
   int act;              // 0 none, 1 relu
   bf16* y;
   int ldy;
-  float* ws;            // split-K partial slabs [splits][M][npad]
+  float* ws;            // split-K partial slabs [splits][tiles][BM*BN]; tile counters in the last 64 KB
   long ws_bytes;
-  int splits, kps, npad;
+  int splits, kps;
+  int* counters;        // [tiles] arrival counts, zero between launches (the workspace starts zeroed)
 };
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of every padded / out-of-range piece
 
 namespace {
+
+// 16-B buffer stores / loads with the sc1 cache policy (device-coherent hand-off between workgroups);
+// the buffer builtins keep the compiler's vmcnt tracking (an inline-asm load would not)
+constexpr int kSc1 = 16;  // CPol::SC1 on gfx94x/gfx950
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void store_sc1_x4(__amdgpu_buffer_rsrc_t r, long off_f, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(off_f * 4), 0, kSc1);
+}
+__device__ __forceinline__ f32x4 load_sc1_x4(__amdgpu_buffer_rsrc_t r, long off_f) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off_f * 4), 0, kSc1);
+}
 
 __device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, int c, float* v, bool add_bias) {
   const bool full = (c + 8 <= p.cout);
@@ -336,18 +350,50 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
 
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   if (p.splits > 1) {
-    // split-K: fp32 partial slab straight from the accumulators (16 lanes = 64 contiguous bytes)
+    // split-K, reduced in-kernel by the tile's last-arriving block (deterministic: partials are summed
+    // in split order).  Partials go out in the accumulator-native layout [split][tile][wave][i][j][lane]
+    // as 16-B sc1 stores; one lane per block then bumps the tile's counter (agent-scope atomic) after
+    // every wave's vmcnt(0); the block that sees splits-1 reads the others back with sc1 loads
+    // (MI355X_MICROARCH.md hand-off table, row 1) and runs the normal epilogue.
+    constexpr int TILE_F = BM * BN;
+    const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
+    const long slab = ((long)blockIdx.y * gridDim.x + lb) * TILE_F + wid * (WM * WN) + lane * 4;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const long m = m0 + wm * WM + i * 16 + row_l + e;
-        if (m >= M) continue;
-        float* dst = p.ws + ((long)blockIdx.y * M + m) * p.npad + n0 + wn * WN + col_l;
+      for (int j = 0; j < NJ; ++j) store_sc1_x4(rs, slab + (i * NJ + j) * 256, acc[i][j]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int s_last;
+    __syncthreads();
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(p.counters + lb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = old == p.splits - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // every split's partial (this block's own included) is read back in split order
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) dst[j * 16] = acc[i][j][e];
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (in row halves of the wave tile, to keep the register peak of the main loop's occupancy)
+    constexpr int MH = MI > 1 ? MI / 2 : 1;
+#pragma unroll
+    for (int i0 = 0; i0 < MI; i0 += MH) {
+      for (int sp = 0; sp < p.splits; ++sp) {
+        const long src = ((long)sp * gridDim.x + lb) * TILE_F + wid * (WM * WN) + lane * 4;
+        f32x4 part[MH][NJ];
+#pragma unroll
+        for (int i = 0; i < MH; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) part[i][j] = load_sc1_x4(rs, src + ((i0 + i) * NJ + j) * 256);
+#pragma unroll
+        for (int i = 0; i < MH; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i0 + i][j] += part[i][j];
       }
-    return;
+    }
+    if (tid == 0) p.counters[lb] = 0;  // ready for the next launch (ordered by the kernel boundary)
   }
 
   // ---- epilogue: bias in fp32, round to bf16 into a per-wave LDS tile, then 16-B coalesced rows
@@ -378,24 +424,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   }
 }
 
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvGemmParams p, long M) {
-  const int gpr = p.npad / 8;
-  const long total = M * gpr;
-  for (long g = blockIdx.x * 256L + threadIdx.x; g < total; g += (long)gridDim.x * 256) {
-    const long m = g / gpr;
-    const int c = (int)(g - m * gpr) * 8;
-    if (c >= p.cout) continue;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int s = 0; s < p.splits; ++s) {
-      const float* src = p.ws + ((long)s * M + m) * p.npad + c;
-      const float4 lo = *reinterpret_cast<const float4*>(src);
-      const float4 hi = *reinterpret_cast<const float4*>(src + 4);
-      v[0] += lo.x; v[1] += lo.y; v[2] += lo.z; v[3] += lo.w;
-      v[4] += hi.x; v[5] += hi.y; v[6] += hi.z; v[7] += hi.w;
-    }
-    epilogue_store(p, m, c, v, true);
-  }
-}
+constexpr long kCounterBytes = 64 * 1024;
+constexpr int kMaxSplitTiles = (int)(kCounterBytes / 4);
 
 // algorithm table: tile (BM, BN), k-chunk BK and ring depth S
 struct Algo {
@@ -405,30 +435,24 @@ constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 
                            {64, 128, 64, 4},   {128, 128, 64, 3}, {128, 128, 32, 3}, {128, 64, 32, 4},
                            {64, 64, 32, 4},    {256, 64, 32, 3},  {128, 128, 64, 2}, {128, 128, 32, 2},
                            {128, 64, 64, 2},   {64, 64, 64, 2},   {256, 128, 32, 2}, {128, 256, 32, 2},
-                           {256, 64, 64, 2}};
+                           {256, 64, 64, 2},   {128, 32, 64, 2},  {64, 32, 64, 2}};
 constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
 
 template <int BM, int BN, int BK, int S>
 int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t stream) {
   const int tiles = (int)((M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
   const int nk = p.ktot / BK;
-  p.npad = ((p.cout + BN - 1) / BN) * BN;
   splits = max(1, min(splits, nk));
-  if (p.ws == nullptr) splits = 1;
-  while (splits > 1 && (long)splits * M * p.npad * 4 > p.ws_bytes) --splits;
+  if (p.ws == nullptr || tiles > kMaxSplitTiles) splits = 1;
+  while (splits > 1 && (long)splits * tiles * BM * BN * 4 > p.ws_bytes - kCounterBytes) --splits;
   p.kps = (nk + splits - 1) / splits;
   splits = (nk + p.kps - 1) / p.kps;
   p.splits = splits;
+  p.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(p.ws) + (p.ws_bytes - kCounterBytes));
   if (smallc)
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true>), dim3(tiles, splits), dim3(256), 0, stream, p);
   else
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, false>), dim3(tiles, splits), dim3(256), 0, stream, p);
-  if (splits > 1) {
-    const long groups = M * (p.npad / 8);
-    const long nbl = (groups + 255) / 256;
-    const int blocks = (int)(nbl < 8192 ? nbl : 8192);
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, stream, p, M);
-  }
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -437,7 +461,9 @@ int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t 
 void auto_algo(long M, int cout, int nk, int& algo, int& splits) {
   auto units = [&](int bm, int bn) { return (int)((M + bm - 1) / bm) * ((cout + bn - 1) / bn); };
   const bool narrow = (cout <= 64) || (((cout + 63) / 64) * 64 < ((cout + 127) / 128) * 128);
-  if (!narrow && units(128, 128) >= 192) {
+  if (cout <= 32) {
+    algo = 17;  // 128x32: output-channel counts like TAESD's final conv (3)
+  } else if (!narrow && units(128, 128) >= 192) {
     algo = 10;  // 128x128, BK 64, double-buffered (2 blocks / CU)
   } else if (units(128, 64) >= 160) {
     algo = 12;  // 128x64, BK 64, double-buffered
@@ -447,7 +473,7 @@ void auto_algo(long M, int cout, int nk, int& algo, int& splits) {
   const Algo a = kAlgos[algo];
   const int u = units(a.bm, a.bn);
   splits = 1;
-  if (u < 160 && nk >= 8) splits = min(min((320 + u - 1) / u, nk / 4), 16);
+  if (u < 160 && nk >= 8) splits = min(min((320 + u - 1) / u, nk / 4), 32);
 }
 
 }  // namespace
@@ -472,8 +498,9 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   p.mask = (const bf16*)d->mask; p.ldmask = d->ldmask;
   p.act = d->act;
   p.y = (bf16*)d->y; p.ldy = d->ldy;
-  p.ws = d->ws; p.ws_bytes = d->ws_bytes;
-  p.splits = 1; p.kps = 0; p.npad = 0;
+  p.ws = d->ws;
+  p.ws_bytes = d->ws_bytes < (1L << 31) ? d->ws_bytes : (1L << 31);  // 32-bit buffer offsets
+  p.splits = 1; p.kps = 0; p.counters = nullptr;
   // shape / alignment contract (host pads channels, see DESIGN.md "layouts")
   if (p.ktot % 64 != 0 || p.ktot < p.kh * p.kw * p.cin) return DC_ERR_ARG;
   if (p.cin % 8 != 0 || p.cout <= 0 || p.nb <= 0 || p.hout <= 0 || p.wout <= 0) return DC_ERR_ARG;
@@ -501,7 +528,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
 #define DC_ALGO(i) \
   case i: return launch_algo<kAlgos[i].bm, kAlgos[i].bn, kAlgos[i].bk, kAlgos[i].s>(p, M, splits, smallc, s);
     DC_ALGO(1) DC_ALGO(2) DC_ALGO(3) DC_ALGO(4) DC_ALGO(5) DC_ALGO(6) DC_ALGO(7) DC_ALGO(8) DC_ALGO(9) DC_ALGO(10)
-    DC_ALGO(11) DC_ALGO(12) DC_ALGO(13) DC_ALGO(14) DC_ALGO(15) DC_ALGO(16)
+    DC_ALGO(11) DC_ALGO(12) DC_ALGO(13) DC_ALGO(14) DC_ALGO(15) DC_ALGO(16) DC_ALGO(17) DC_ALGO(18)
 #undef DC_ALGO
     default: return DC_ERR_ARG;
   }

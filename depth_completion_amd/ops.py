@@ -79,7 +79,8 @@ class Ctx:
 
     def __init__(self, device, ws_mb: int = 96, tune: bool | None = None):
         self.device = torch.device(device)
-        self.ws = torch.empty(ws_mb * (1 << 20) // 4, dtype=torch.float32, device=self.device)
+        # zero-filled: the split-K tile counters at its end must start at 0 (dc_conv_gemm keeps them so)
+        self.ws = torch.zeros(ws_mb * (1 << 20) // 4, dtype=torch.float32, device=self.device)
         self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.algo_cache: dict = load_tuned()
         self.tune = os.environ.get("DC_TUNE") == "1" if tune is None else tune
@@ -155,7 +156,7 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3) -> tuple:
     dt = ConvDesc.from_buffer_copy(d)
     dt.y = tmp.data_ptr() + (d.y - base)
     nalg = _lib.load().dc_conv_num_algos()
-    cands = [(0, 0)] + [(a, s) for a in range(1, nalg + 1) for s in (1, 2, 4, 8)]
+    cands = [(0, 0)] + [(a, s) for a in range(1, nalg + 1) for s in (1, 2, 4, 8, 12, 16, 24, 32)]
     best, best_t = (0, 0), float("inf")
     for a, s in cands:
         dt.algo, dt.splitk = a, s

@@ -295,7 +295,7 @@ def test_geglu_and_upsample_adjoint(ctx):
         assert rel(nchw(out, 2, hl, wl), x.grad) < 1e-2
 
 
-@pytest.mark.parametrize("algo", list(range(1, 17)))
+@pytest.mark.parametrize("algo", list(range(1, 19)))
 @pytest.mark.parametrize("nsplit", [1, 3])
 def test_conv_all_algos(ctx, algo, nsplit):
     """every tile / ring variant and split-K on conv (incl. concat, stride 2, upsample) and linear."""

@@ -56,7 +56,7 @@ def main():
 
         flops = 2.0 * nb * ho * wo * cout * k * k * cin
         res = []
-        for algo, ns in [(0, 0)] + [(a, s) for a in range(1, NALG + 1) for s in (1, 2, 4, 8)]:
+        for algo, ns in [(0, 0)] + [(a, s) for a in range(1, NALG + 1) for s in (1, 2, 4, 8, 16)]:
             def run():
                 ops.conv_gemm(ctx, x, wt, nb=nb, hin=hin, win=win, cin=cin, hout=ho, wout=wo, cout=cout, kh=k,
                               kw=k, stride=stride, pad=k // 2, mode=mode, bias=b, y=y, algo=algo, nsplit=ns)
