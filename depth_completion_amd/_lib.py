@@ -6,9 +6,11 @@ if it is missing or was built for another ABI, every hot-path entry point raises
 from __future__ import annotations
 
 import ctypes as C
+import os
 from pathlib import Path
 
-_LIB_PATH = Path(__file__).resolve().parent / "libdcamd.so"
+# DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
+_LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
 ABI_VERSION = 3
 
 vp = C.c_void_p

@@ -345,6 +345,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
 #pragma unroll
         for (int jj = 0; jj < NJ; ++jj)
           acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][ii], bfr[ks][jj], acc[ii][jj], 0, 0, 0);
+    // keep every fragment read of the chunk ahead of its MFMAs (the default schedule interleaves
+    // read -> lgkmcnt(0) -> 2 MFMAs, exposing the LDS latency once per fragment)
+    __builtin_amdgcn_sched_group_barrier(0x100, KS * (MI + NJ), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, KS * MI * NJ, 0);
   }
   vm_wait<0>();
 
@@ -363,14 +367,16 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
 #pragma unroll
       for (int j = 0; j < NJ; ++j) store_sc1_x4(rs, slab + (i * NJ + j) * 256, acc[i][j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __shared__ int s_last;
+    // the flag lives in the (now idle) ring: a second __shared__ object would make the compiler's
+    // waitcnt pass treat every LDS-DMA as aliasing the main loop's ds_reads (vmcnt(0) per chunk)
+    int* s_last = reinterpret_cast<int*>(smem);
     __syncthreads();
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(p.counters + lb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_last = old == p.splits - 1;
+      *s_last = old == p.splits - 1;
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!*s_last) return;
     // every split's partial (this block's own included) is read back in split order
 #pragma unroll
     for (int i = 0; i < MI; ++i)

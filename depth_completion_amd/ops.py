@@ -53,7 +53,7 @@ def LD(t) -> int:
     return t.ld if isinstance(t, Slice) else t.shape[-1]
 
 
-TUNED_TABLE = Path(__file__).resolve().parent / "tuned_gfx950.json"
+TUNED_TABLE = Path(os.environ.get("DC_TUNED") or Path(__file__).resolve().parent / "tuned_gfx950.json")
 
 
 def load_tuned(path: Path = TUNED_TABLE) -> dict:
