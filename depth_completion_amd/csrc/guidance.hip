@@ -383,8 +383,10 @@ __global__ void latent_init_kernel(const bf16* noise, const bf16* prev, float be
 }
 
 // final dense depth: [nb][1][H][W] fp32 metres
+// mode 0: learned affine s^2 (max_g - min_g) aff + sh^2 min_g (marigold_dc.py:323-331);
+// mode 1: closed-form scale * aff + shift (marigold_dc.py:332-336), affine from dc_closed_form_affine
 __global__ void final_dense_kernel(const bf16* out, int ldo, int nb, int PH, int PW, int RH, int RW, int H, int W,
-                                   const float* params, const float* affine, float* dense) {
+                                   const float* params, const float* affine, int mode, float* dense) {
   const long total = (long)nb * H * W;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int x = (int)(i % W);
@@ -394,10 +396,75 @@ __global__ void final_dense_kernel(const bf16* out, int ldo, int nb, int PH, int
     const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t);
     const float* pr = params + n * 8;
     const float s = affine[n * 2], sh = affine[n * 2 + 1];
-    const float B = (s * s) * (pr[5] - pr[4]);
-    const float F = B * aff + (sh * sh) * pr[4];
+    float F;
+    if (mode == 0) {
+      const float B = (s * s) * (pr[5] - pr[4]);
+      F = B * aff + (sh * sh) * pr[4];
+    } else {
+      F = s * aff + sh;
+    }
     const float G = fminf(fmaxf(F, 0.0f), 1.0f);
     dense[i] = G * (pr[1] - pr[0]) + pr[0];
+  }
+}
+
+// Plain DDIM step (train_latents=False, marigold_dc.py:905-909): DDIMScheduler.step(v, t, x).prev_sample
+// on bf16 tensors, eta = 0, with torch's per-op bf16 rounding (same sequence as latent_update's).
+__global__ void ddim_step_kernel(bf16* x8, const bf16* v, long total, const float* coef, const int* step) {
+  const int st = *step;
+  const float sa = coef[st * 4 + 0], sb = coef[st * 4 + 1], sap = coef[st * 4 + 2], sbp = coef[st * 4 + 3];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const long pix = i >> 2;
+    const int k = (int)(i & 3);
+    const float xp = (float)x8[pix * 8 + 4 + k];
+    const float vm = (float)v[pix * 8 + k];
+    const float x0 = (float)(bf16)((float)(bf16)(sa * xp) - (float)(bf16)(sb * vm));
+    const float ep = (float)(bf16)((float)(bf16)(sa * vm) + (float)(bf16)(sb * xp));
+    const float dir = (float)(bf16)(sbp * ep);
+    x8[pix * 8 + 4 + k] = (bf16)((float)(bf16)(sap * x0) + dir);
+  }
+}
+
+// compute_affine_params (marigold_dc.py:53-128) over the sparse pixels only (the mask is zero elsewhere),
+// one block per frame, with the reference's dtype placement: the affine map is bf16, so its masked sum,
+// mean, centred values, squares and variance are bf16-rounded; guides and the covariance are fp32.
+__global__ void closed_form_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
+                                   const int* idx, const float* gval, const int* cnt, float* affine) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.x;
+  const long HW = (long)H * W;
+  const int count = cnt[n];
+  const int* ix = idx + n * HW;
+  const float* gv = gval + n * HW;
+  auto aff_at = [&](int k) {
+    const int p = ix[k];
+    Taps t;
+    return sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t);
+  };
+  float sa = 0.0f, sg = 0.0f;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    sa += aff_at(k);
+    sg += gv[k];
+  }
+  const float sum_a = (float)(bf16)block_sum(sa, scratch);
+  __syncthreads();
+  const float sum_g = block_sum(sg, scratch);
+  __syncthreads();
+  const float ma = (float)(bf16)(sum_a / (float)count);
+  const float mg = sum_g / (float)count;
+  float sv = 0.0f, sc = 0.0f;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    const float ac = (float)(bf16)(aff_at(k) - ma);
+    sv += (float)(bf16)(ac * ac);
+    sc += ac * (gv[k] - mg);
+  }
+  const float var = (float)(bf16)block_sum(sv, scratch);
+  __syncthreads();
+  const float cov = block_sum(sc, scratch);
+  if (threadIdx.x == 0) {
+    const float scale = cov / (float)(bf16)(var + 1e-7f);
+    affine[n * 2] = scale;
+    affine[n * 2 + 1] = mg - scale * ma;
   }
 }
 
@@ -481,10 +548,30 @@ extern "C" int dc_latent_init(const void* noise, const void* prev, float beta, i
 }
 
 extern "C" int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
-                              const float* params, const float* affine, float* dense, void* stream) {
-  if (!dec_out || !params || !affine || !dense || nb <= 0) return DC_ERR_ARG;
+                              const float* params, const float* affine, int mode, float* dense, void* stream) {
+  if (!dec_out || !params || !affine || !dense || nb <= 0 || mode < 0 || mode > 1) return DC_ERR_ARG;
   hipLaunchKernelGGL(final_dense_kernel, grid_for((long)nb * h * w), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)dec_out, ldo, nb, ph, pw, rh, rw, h, w, params, affine, dense);
+                     (const bf16*)dec_out, ldo, nb, ph, pw, rh, rw, h, w, params, affine, mode, dense);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_ddim_step(void* x8, const void* v, int nb, int hw, const float* coef, const int* step,
+                            void* stream) {
+  if (!x8 || !v || !coef || !step || nb <= 0 || hw <= 0) return DC_ERR_ARG;
+  const long total = (long)nb * hw * 4;
+  hipLaunchKernelGGL(ddim_step_kernel, grid_for(total), dim3(256), 0, (hipStream_t)stream, (bf16*)x8,
+                     (const bf16*)v, total, coef, step);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_closed_form_affine(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h,
+                                     int w, const int* idx, const float* gval, const int* cnt, float* affine,
+                                     void* stream) {
+  if (!dec_out || !idx || !gval || !cnt || !affine || nb <= 0) return DC_ERR_ARG;
+  hipLaunchKernelGGL(closed_form_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
+                     pw, rh, rw, h, w, idx, gval, cnt, affine);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

@@ -172,16 +172,19 @@ class MarigoldDepthCompletionPipeline:
         lr_latent, lr_scaling = (0.05, 0.005) if lr is None else lr
         loss_funcs = ["l1", "l2"] if loss_funcs is None else list(loss_funcs)
         # the hot path of this build (SURVEY.md §8 defaults); other modes are §8(f) "next" rows
+        # train_latents=False (+ closed form) is the plain DDIM sampler with the closed-form fit at the end
+        # (marigold_dc.py:905-909, 969-985): no optimiser, loss or guidance settings take part in it
+        guided = train_latents
         unsupported = []
-        if closed_form or not train_latents:
-            unsupported.append("closed_form / train_latents=False")
-        if train_method != "per-step":
+        if guided and closed_form:
+            unsupported.append("closed_form with train_latents=True")
+        if guided and train_method != "per-step":
             unsupported.append("train_method=per-input")
-        if opt != "adam":
+        if guided and opt != "adam":
             unsupported.append(f"opt={opt}")
-        if kld:
+        if guided and kld:
             unsupported.append("kld")
-        if sorted(loss_funcs) != ["l1", "l2"]:
+        if guided and sorted(loss_funcs) != ["l1", "l2"]:
             unsupported.append(f"loss_funcs={loss_funcs}")
         if interp_mode != "bilinear":
             unsupported.append(f"interp_mode={interp_mode}")
@@ -239,7 +242,7 @@ class MarigoldDepthCompletionPipeline:
         if (cnt_host == 0).any():
             raise ValueError("No valid values found in mask for some positions. "
                              "Ensure that mask has at least one True value along the specified dimensions.")
-        if projection != "linear" or inv:
+        if guided and (projection != "linear" or inv):
             raise NotImplementedError("non-linear depth space in the loss is a next-round row (SURVEY §8f)")
 
         # ---- per-call tables
@@ -254,10 +257,11 @@ class MarigoldDepthCompletionPipeline:
         self._call_state = dict(idx=idx, gval=gval, cnt=cnt, params=params, coef=coef, adam=adam, H=H, W=W, RH=RH,
                                 RW=RW, PH=PH, PW=PW, n=n, h=h, w=w)
 
-        # ---- guided denoising loop (marigold_dc.py:800-904)
+        # ---- denoising loop (marigold_dc.py:800-909): guided steps, or plain DDIM steps
+        step_fn = self._step if guided else self._ddim_step
         if self.use_graph:
             g = st["graph"]
-            gkey = (steps, H, W, RH, RW, lr_latent, lr_scaling)
+            gkey = (guided, steps, H, W, RH, RW, lr_latent, lr_scaling)
             if g is None or st["graph_key"] != gkey:
                 # tables are rebuilt per call at new addresses: capture against this call's buffers
                 g = torch.cuda.CUDAGraph()
@@ -265,13 +269,13 @@ class MarigoldDepthCompletionPipeline:
                 s = torch.cuda.Stream(dev)
                 s.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(s):
-                    self._step(st)      # warm-up on a side stream (first-use lazy init)
+                    step_fn(st)         # warm-up on a side stream (first-use lazy init)
                 torch.cuda.current_stream(dev).wait_stream(s)
                 torch.cuda.synchronize(dev)
                 # undo the warm-up step's state change
                 self._reset_state(st, n, noise, prev, beta)
                 with torch.cuda.graph(g):
-                    self._step(st)
+                    step_fn(st)
                 st["graph"], st["graph_key"] = g, gkey
                 st["graph_tables"] = (coef, adam, idx, gval, cnt, params)
             else:
@@ -283,15 +287,18 @@ class MarigoldDepthCompletionPipeline:
                 g.replay()
         else:
             for _ in range(steps):
-                self._step(st)
+                step_fn(st)
 
         # ---- final decode (marigold_dc.py:969-985)
         _lib.call("dc_taesd_clamp_fwd", ops.P(ops.Slice(up.x8, 4)), 8, P, dp.tin.data_ptr(), ctx.stream)
         dp.forward()
         dense = torch.empty(n, 1, H, W, dtype=torch.float32, device=dev)
         cs = self._tables(st)
+        if closed_form:   # compute_affine_params on the final decode (marigold_dc.py:332-336)
+            _lib.call("dc_closed_form_affine", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["idx"].data_ptr(),
+                      cs["gval"].data_ptr(), cs["cnt"].data_ptr(), st["affine"].data_ptr(), ctx.stream)
         _lib.call("dc_final_dense", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["params"].data_ptr(),
-                  st["affine"].data_ptr(), dense.data_ptr(), ctx.stream)
+                  st["affine"].data_ptr(), int(bool(closed_form)), dense.data_ptr(), ctx.stream)
         lat = torch.empty(n, 4, h, w, dtype=BF16, device=dev)
         _lib.call("dc_nhwc_to_nchw", ops.P(ops.Slice(up.x8, 4)), 8, n, h * w, 4, lat.data_ptr(), ctx.stream)
         self.last_loss = st["loss"]
@@ -313,6 +320,18 @@ class MarigoldDepthCompletionPipeline:
             ops.memset(ctx, t)
         st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))
         ops.memset(ctx, ctx.step)
+
+    def _ddim_step(self, st):
+        """One plain DDIM step (train_latents=False, marigold_dc.py:905-909): UNet forward + prev_sample."""
+        ctx = self.ctx
+        cs = self._tables(st)
+        up = st["unet"]
+        n, h, w = cs["n"], cs["h"], cs["w"]
+        step = ctx.step.data_ptr()
+        up.forward()
+        _lib.call("dc_ddim_step", up.x8.data_ptr(), up.v.data_ptr(), n, h * w, cs["coef"].data_ptr(), step,
+                  ctx.stream)
+        _lib.call("dc_step_advance", step, int(cs["coef"].shape[0]), ctx.stream)
 
     def _step(self, st):
         """One guided DDIM step (marigold_dc.py:802-904) as a flat launch sequence."""

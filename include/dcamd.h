@@ -136,7 +136,13 @@ int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gune
 int dc_step_advance(int* step, int nsteps, void* stream);  /* saturates at nsteps-1 */
 int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8, void* stream);
 int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
-                   const float* params, const float* affine, float* dense, void* stream);
+                   const float* params, const float* affine, int mode, float* dense, void* stream);
+/* mode 0 learned affine (marigold_dc.py:323-331), 1 closed form (:332-336) */
+/* plain DDIM step, train_latents=False (marigold_dc.py:905-909): x8[...,4:8] <- prev_sample(v, x) */
+int dc_ddim_step(void* x8, const void* v, int nb, int hw, const float* coef, const int* step, void* stream);
+/* compute_affine_params (marigold_dc.py:53-128) over the sparse pixels: affine[nb][2] = scale, shift */
+int dc_closed_form_affine(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                          const int* idx, const float* gval, const int* cnt, float* affine, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
 
 #ifdef __cplusplus

@@ -132,3 +132,32 @@ def test_errors_match_reference():
         pipe(imgs, sparses, 120.0, closed_form=False, train_latents=False)
     with pytest.raises(ValueError):  # empty mask (utils.py:132-136)
         pipe(imgs, torch.zeros_like(sparses), 120.0, resolution=64, steps=1)
+
+
+@pytest.mark.parametrize("kw", [dict(norm="const"), dict(norm="minmax", projection="log10", min_depth=1.0),
+                                dict(norm="minmax", inv=True, min_depth=1.0)])
+def test_plain_ddim_closed_form(kw):
+    """train_latents=False: plain DDIM + closed-form affine on the final decode (marigold_dc.py:905-909,
+    332-336, 969-985), the mode of the golden case closed_form_fp32 that pins the oracle."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    n, h, w, res, steps = 2, 48, 64, 64, 8
+    cfg_o = tiny_unet_config()
+    imgs, sparses = synth_inputs(n, h, w, 60, seed=17)
+    noise = torch.randn((1, 4, 6, 8), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
+    args = dict(kw, steps=steps, resolution=res, init_noise=noise, train_latents=False)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
+    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
+    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dh).all()
+    rng = (d32.amax(dim=(1, 2, 3)) - d32.amin(dim=(1, 2, 3))).view(-1, 1, 1, 1)
+    err_h = float(((dh - d32).abs() / rng).mean())
+    err_b = float(((d16 - d32).abs() / rng).mean())
+    lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
+    lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
+    print(f"\nplain DDIM {kw}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
+    assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
