@@ -1,4 +1,4 @@
-import os
+import os  # noqa: F401
 import sys
 from pathlib import Path
 
