@@ -13,6 +13,10 @@
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
+
+// raw v_exp_f32: exp2f() wraps it in a denormal-range fix-up (cmp/cndmask/add/ldexp, ~6 VALU per
+// call), pure overhead for softmax weights, where results below 2^-126 may flush to zero
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 constexpr int KSTR = 72;   // row stride (elements) of row-read tiles: 144 B, conflict-free ds_read_b128
 constexpr int VSTR = 96;   // row stride of tr-read-only tiles: 192 B, conflict-free ds_read_b64_tr_b16
 
@@ -195,12 +199,12 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_fwd_kernel(const bf16* qkv,
         for (int b = 0; b < 2; ++b)
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float pv = exp2f(fmaf(sacc[b][r], LOG2E, -ml));
+            const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
             sacc[b][r] = pv;
             ps += pv;
           }
         if (__any(mnew > m)) {
-          const float alpha = exp2f((m - mnew) * LOG2E);
+          const float alpha = fast_exp2((m - mnew) * LOG2E);
           l *= alpha;
   #pragma unroll
           for (int db = 0; db < 2; ++db)
@@ -248,7 +252,7 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_fwd_kernel(const bf16* qkv,
       const float* src = red + ((p - 1) * 4 + wid) * 34 * 64 + lane;
       const float mp = src[0], lp = src[64];
       const float mn = fmaxf(m, mp);
-      const float a0 = exp2f((m - mn) * LOG2E), a1 = exp2f((mp - mn) * LOG2E);
+      const float a0 = fast_exp2((m - mn) * LOG2E), a1 = fast_exp2((mp - mn) * LOG2E);
       l = l * a0 + lp * a1;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dkdv_kernel(const bf16*
           // sp = S - lse -> P ; dp = dP - delta -> dS = P * dp
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float pv = exp2f(sp[r] * LOG2E);
+            const float pv = fast_exp2(sp[r] * LOG2E);
             sp[r] = pv;
             dp[r] = pv * dp[r];
           }
@@ -554,7 +558,7 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dq_kernel(const bf16* q
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const float pv = key < T ? exp2f(sp[r] * LOG2E - my_lse) : 0.0f;
+            const float pv = key < T ? fast_exp2(sp[r] * LOG2E - my_lse) : 0.0f;
             sp[r] = pv * (dp[r] - my_del);  // dS^T
           }
   #pragma unroll
