@@ -111,7 +111,7 @@ struct FwdLds {
 };
 
 template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) void attn_fwd_kernel(const bf16* qkv, int ld, int T, int heads, bf16* o,
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(const bf16* qkv, int ld, int T, int heads, bf16* o,
                                                             int ldo, float* lse) {
   __shared__ __attribute__((aligned(16))) char smem[FwdLds<QW, KS>::BYTES];
   constexpr int NT = 64 * QW;  // threads per key/query split
@@ -311,7 +311,7 @@ struct DkdvLds {
 };
 
 template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dkdv_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
                                                                  const float* lse, const float* delta, int T,
                                                                  int heads, bf16* dqkv, int ldd) {
   __shared__ __attribute__((aligned(16))) char smem[DkdvLds<QW, KS>::BYTES];
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dkdv_kernel(const bf16*
     stage_load<NT>(dob, lddo, qt * 64, T, h * 64, r.d, lt);
     if (lt < 64) {
       const int q = qt * 64 + lt;
-      r.l = q < T ? lse_b[q] : INFINITY;
+      r.l = q < T ? lse_b[q] * LOG2E : INFINITY;  // consumed as exp2(S log2e - lse log2e)
       r.dl = q < T ? del_b[q] : 0.0f;
     }
   };
@@ -387,13 +387,9 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dkdv_kernel(const bf16*
         const bf16* dt_s = ds_ + cur * 64 * KSTR;
   #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
-          f32x16 sp, dp;
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int qr = 32 * qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            sp[r] = -ls[cur * 64 + qr];
-            dp[r] = -dl[cur * 64 + qr];
-          }
+          // S and dP from zero accumulators; lse (pre-scaled by log2 e) and delta are read 4 rows per
+          // ds_read_b128: accumulator element r holds query row 32 qb + 8 (r >> 2) + 4 hh + (r & 3)
+          f32x16 sp = {}, dp = {};
   #pragma unroll
           for (int s = 0; s < 4; ++s) {
             const bf16x8 qa =
@@ -403,12 +399,17 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dkdv_kernel(const bf16*
                 *reinterpret_cast<const bf16x8*>(dt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
             dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
           }
-          // sp = S - lse -> P ; dp = dP - delta -> dS = P * dp
+          // P = exp2(S log2e - lse log2e); dS = P * (dP - delta)
   #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float pv = fast_exp2(sp[r] * LOG2E);
-            sp[r] = pv;
-            dp[r] = pv * dp[r];
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + cur * 64 + 32 * qb + 8 * g + 4 * hh);
+            const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + cur * 64 + 32 * qb + 8 * g + 4 * hh);
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float pv = fast_exp2(fmaf(sp[4 * g + e], LOG2E, -l4[e]));
+              sp[4 * g + e] = pv;
+              dp[4 * g + e] = pv * (dp[4 * g + e] - d4[e]);
+            }
           }
   #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
@@ -486,7 +487,7 @@ struct DqLds {
 };
 
 template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dq_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
                                                                const float* lse, const float* delta, int T, int heads,
                                                                bf16* dqkv, int ldd) {
   __shared__ __attribute__((aligned(16))) char smem[DqLds<QW, KS>::BYTES];
@@ -557,9 +558,13 @@ __global__ __launch_bounds__(64 * QW * KS) void attn_bwd_dq_kernel(const bf16* q
           }
   #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const float pv = key < T ? fast_exp2(sp[r] * LOG2E - my_lse) : 0.0f;
+            const float pv = fast_exp2(fmaf(sp[r], LOG2E, -my_lse));
             sp[r] = pv * (dp[r] - my_del);  // dS^T
+          }
+          if ((kt + 1) * 64 > T) {  // keys beyond T exist only in the last tile
+  #pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) sp[r] = 0.0f;
           }
   #pragma unroll
           for (int s2 = 0; s2 < 2; ++s2) {
