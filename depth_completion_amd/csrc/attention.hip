@@ -625,6 +625,8 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 // attn2(LN2(x)) with a constant 2-token context reduces exactly to
 //   out = x + c0 + sum_h sigmoid(LN2(x) . U_h) * D_h        (U, D: [H][C] fp32, c0: [C] fp32)
 // (U_h = Wq_h^T (k1_h - k2_h)/8, D_h = Wo_h (v1_h - v2_h), c0 = Wo v2 + bo).
+constexpr int kCrossMaxHeads = 20;  // SD2 UNet: 5 / 10 / 20 heads
+
 template <int MAXV>
 __global__ void cross_fwd_kernel(const bf16* x, int ldx, long rows, int c, int heads, float eps, const float* gamma,
                                  const float* beta, const float* U, const float* D, const float* c0, bf16* y, int ldy,
@@ -664,30 +666,50 @@ __global__ void cross_fwd_kernel(const bf16* x, int ldx, long rows, int c, int h
         nn[k][i] = (float)(bf16)((xv[k][i] - mu) * rs * gamma[vi * 8 + i] + beta[vi * 8 + i]);
     }
   }
+  // all heads' logits in one pass over the row, reduced together (independent butterflies), then the
+  // sigmoid-weighted sum of the D rows
+  float d[kCrossMaxHeads];
+#pragma unroll
+  for (int hd = 0; hd < kCrossMaxHeads; ++hd) d[hd] = 0.0f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nv) {
+#pragma unroll
+      for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
+        if (hd < heads) {
+          const float4* u = reinterpret_cast<const float4*>(U + (long)hd * c + vi * 8);
+          const float4 u0 = u[0], u1 = u[1];
+          d[hd] += nn[k][0] * u0.x + nn[k][1] * u0.y + nn[k][2] * u0.z + nn[k][3] * u0.w + nn[k][4] * u1.x +
+                   nn[k][5] * u1.y + nn[k][6] * u1.z + nn[k][7] * u1.w;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+    for (int hd = 0; hd < kCrossMaxHeads; ++hd)
+      if (hd < heads) d[hd] += __shfl_xor(d[hd], o, 64);
   float acc[MAXV][8];
 #pragma unroll
   for (int k = 0; k < MAXV; ++k)
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[k][i] = 0.0f;
-  for (int hd = 0; hd < heads; ++hd) {
-    float d = 0.0f;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-      const int vi = lane + 64 * k;
-      if (vi < nv) {
+  for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
+    if (hd < heads) {
+      const float p = 1.0f / (1.0f + __expf(-d[hd]));
+      if (lane == 0) probs[row * heads + hd] = p;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) d += nn[k][i] * U[(long)hd * c + vi * 8 + i];
-      }
-    }
-    d = wave_sum(d);
-    const float p = 1.0f / (1.0f + __expf(-d));
-    if (lane == 0) probs[row * heads + hd] = p;
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-      const int vi = lane + 64 * k;
-      if (vi < nv) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[k][i] += p * D[(long)hd * c + vi * 8 + i];
+      for (int k = 0; k < MAXV; ++k) {
+        const int vi = lane + 64 * k;
+        if (vi < nv) {
+          const float4* dd = reinterpret_cast<const float4*>(D + (long)hd * c + vi * 8);
+          const float4 d0 = dd[0], d1 = dd[1];
+          acc[k][0] += p * d0.x; acc[k][1] += p * d0.y; acc[k][2] += p * d0.z; acc[k][3] += p * d0.w;
+          acc[k][4] += p * d1.x; acc[k][5] += p * d1.y; acc[k][6] += p * d1.z; acc[k][7] += p * d1.w;
+        }
       }
     }
   }
@@ -723,25 +745,43 @@ __global__ void cross_bwd_kernel(const bf16* x, int ldx, long rows, int c, int h
     for (int i = 0; i < 8; ++i) dn[k][i] = 0.0f;
     if (vi < nv) load8(dy + row * lddy + vi * 8, dv[k]);
   }
-  for (int hd = 0; hd < heads; ++hd) {
-    float d = 0.0f;
+  float d[kCrossMaxHeads];
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-      const int vi = lane + 64 * k;
-      if (vi < nv) {
+  for (int hd = 0; hd < kCrossMaxHeads; ++hd) d[hd] = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) d += dv[k][i] * D[(long)hd * c + vi * 8 + i];
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nv) {
+#pragma unroll
+      for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
+        if (hd < heads) {
+          const float4* dd = reinterpret_cast<const float4*>(D + (long)hd * c + vi * 8);
+          const float4 d0 = dd[0], d1 = dd[1];
+          d[hd] += dv[k][0] * d0.x + dv[k][1] * d0.y + dv[k][2] * d0.z + dv[k][3] * d0.w + dv[k][4] * d1.x +
+                   dv[k][5] * d1.y + dv[k][6] * d1.z + dv[k][7] * d1.w;
+        }
       }
     }
-    d = wave_sum(d);
-    const float p = probs[row * heads + hd];
-    const float dsg = d * p * (1.0f - p);
+  }
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-      const int vi = lane + 64 * k;
-      if (vi < nv) {
+  for (int o = 32; o >= 1; o >>= 1)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) dn[k][i] += dsg * U[(long)hd * c + vi * 8 + i];
+    for (int hd = 0; hd < kCrossMaxHeads; ++hd)
+      if (hd < heads) d[hd] += __shfl_xor(d[hd], o, 64);
+#pragma unroll
+  for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
+    if (hd < heads) {
+      const float p = probs[row * heads + hd];
+      const float dsg = d[hd] * p * (1.0f - p);
+#pragma unroll
+      for (int k = 0; k < MAXV; ++k) {
+        const int vi = lane + 64 * k;
+        if (vi < nv) {
+          const float4* u = reinterpret_cast<const float4*>(U + (long)hd * c + vi * 8);
+          const float4 u0 = u[0], u1 = u[1];
+          dn[k][0] += dsg * u0.x; dn[k][1] += dsg * u0.y; dn[k][2] += dsg * u0.z; dn[k][3] += dsg * u0.w;
+          dn[k][4] += dsg * u1.x; dn[k][5] += dsg * u1.y; dn[k][6] += dsg * u1.z; dn[k][7] += dsg * u1.w;
+        }
       }
     }
   }
@@ -885,7 +925,8 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
 extern "C" int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps,
                                 const float* gamma, const float* beta, const float* U, const float* D,
                                 const float* c0, void* y, int ldy, float* stats, float* probs, void* stream) {
-  if (!x || !y || !gamma || !beta || !U || !D || !c0 || !stats || !probs || rows <= 0 || c % 8 || heads <= 0)
+  if (!x || !y || !gamma || !beta || !U || !D || !c0 || !stats || !probs || rows <= 0 || c % 8 || heads <= 0 ||
+      heads > kCrossMaxHeads)
     return DC_ERR_ARG;
   if (ldx % 8 || ldy % 8) return DC_ERR_ALIGN;
   DC_CROSS_DISPATCH(cross_fwd_kernel, (const bf16*)x, ldx, (long)rows, c, heads, eps, gamma, beta, U, D, c0, (bf16*)y,
@@ -897,7 +938,8 @@ extern "C" int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, i
 extern "C" int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, int heads, const float* gamma,
                                 const float* U, const float* D, const float* stats, const float* probs,
                                 const void* dy, int lddy, void* dx, int lddx, void* stream) {
-  if (!x || !dy || !dx || !gamma || !U || !D || !stats || !probs || rows <= 0 || c % 8 || heads <= 0)
+  if (!x || !dy || !dx || !gamma || !U || !D || !stats || !probs || rows <= 0 || c % 8 || heads <= 0 ||
+      heads > kCrossMaxHeads)
     return DC_ERR_ARG;
   if (ldx % 8 || lddy % 8 || lddx % 8) return DC_ERR_ALIGN;
   DC_CROSS_DISPATCH(cross_bwd_kernel, (const bf16*)x, ldx, (long)rows, c, heads, gamma, U, D, stats, probs,
