@@ -19,6 +19,7 @@ struct GNShape {
   int ldx, ldx2, c1;
   int nb, hw, c, groups, cpg;
   int rows_per_chunk, nchunk;
+  int apply_rows;  // rows per block of the elementwise passes
   int cgs, R;  // colgroups (c/8) and parallel rows per block
 };
 
@@ -111,24 +112,34 @@ __global__ void gn_finalize_kernel(GNShape s, const float* part, float eps, int 
   }
 }
 
+// Elementwise passes: block (chunk, frame) with the stats kernel's thread layout -- each thread keeps
+// one 8-channel group (cg = tid % cgs) over rows r0, r0 + R, ... -- so the per-channel coefficients
+// are computed once per thread and the row loop carries no divisions.
 __global__ void gn_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
                                 bf16* y, int ldy) {
-  const long total = (long)s.nb * s.hw * s.cgs;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % s.cgs);
-    const long pix = i / s.cgs;
-    const int n = (int)(pix / s.hw), row = (int)(pix - (long)n * s.hw);
+  const int n = blockIdx.y;
+  const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
+  if (r0 >= s.R) return;
+  float mu[8], rs[8], ga[8], be[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = cg * 8 + k, g = c / s.cpg;
+    mu[k] = stats[((long)n * s.groups + g) * 2];
+    rs[k] = stats[((long)n * s.groups + g) * 2 + 1];
+    ga[k] = gamma[c];
+    be[k] = beta[c];
+  }
+  const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows);
+  for (int row = rbeg + r0; row < rend; row += s.R) {
     float f[8];
     gn_load8(s, n, row, cg * 8, f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = cg * 8 + k, g = c / s.cpg;
-      const float mu = stats[((long)n * s.groups + g) * 2], rs = stats[((long)n * s.groups + g) * 2 + 1];
-      float v = (f[k] - mu) * rs * gamma[c] + beta[c];
+      float v = (f[k] - mu[k]) * rs[k] * ga[k] + be[k];
       if (silu) v = silu_f((float)(bf16)v);
       f[k] = v;
     }
-    store8(y + pix * ldy + cg * 8, f);
+    store8(y + ((long)n * s.hw + row) * ldy + cg * 8, f);
   }
 }
 
@@ -176,18 +187,35 @@ __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* 
 __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
                                     const bf16* dy, int lddy, const float* ab, bf16* dx, int lddx,
                                     const bf16* add1, int ldadd1, const bf16* add2, int ldadd2) {
-  const long total = (long)s.nb * s.hw * s.cgs;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % s.cgs);
-    const long pix = i / s.cgs;
-    const int n = (int)(pix / s.hw), row = (int)(pix - (long)n * s.hw);
-    float xh[8], gdy[8], rs[8], out[8];
-    gn_bwd_elem(s, n, row, cg, stats, gamma, beta, silu, dy, lddy, xh, gdy, rs);
+  const int n = blockIdx.y;
+  const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
+  if (r0 >= s.R) return;
+  float mu[8], rs[8], ga[8], be[8], ma[8], mb[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = cg * 8 + k, g = c / s.cpg;
+    mu[k] = stats[((long)n * s.groups + g) * 2];
+    rs[k] = stats[((long)n * s.groups + g) * 2 + 1];
+    ma[k] = ab[((long)n * s.groups + g) * 2];
+    mb[k] = ab[((long)n * s.groups + g) * 2 + 1];
+    ga[k] = gamma[c];
+    be[k] = beta[c];
+  }
+  const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows);
+  for (int row = rbeg + r0; row < rend; row += s.R) {
+    const long pix = (long)n * s.hw + row;
+    float f[8], d[8], out[8];
+    gn_load8(s, n, row, cg * 8, f);
+    load8(dy + pix * lddy + cg * 8, d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int g = (cg * 8 + k) / s.cpg;
-      const float ma = ab[((long)n * s.groups + g) * 2], mb = ab[((long)n * s.groups + g) * 2 + 1];
-      out[k] = rs[k] * (gdy[k] - ma - xh[k] * mb);
+      const float xhat = (f[k] - mu[k]) * rs[k];
+      float dd = d[k];
+      if (silu) {
+        const float yv = (float)(bf16)(xhat * ga[k] + be[k]);
+        dd = (float)(bf16)(dd * silu_grad(yv));
+      }
+      out[k] = rs[k] * (dd * ga[k] - ma[k] - xhat * mb[k]);
     }
     if (add1) {
       float e[8];
@@ -227,17 +255,15 @@ bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2,
   s.rows_per_chunk = max(s.R, (hw + target_blocks - 1) / target_blocks);
   s.rows_per_chunk = ((s.rows_per_chunk + s.R - 1) / s.R) * s.R;
   s.nchunk = (hw + s.rows_per_chunk - 1) / s.rows_per_chunk;
+  // elementwise passes: ~1024 blocks over the launch, at least R and at most 64 rows per block
+  const int bpf = max(1, 1024 / nb);
+  s.apply_rows = min(64, max(s.R, (hw + bpf - 1) / bpf));
+  s.apply_rows = ((s.apply_rows + s.R - 1) / s.R) * s.R;
   return true;
 }
 
 // workspace layout: [partials nb*nchunk*G*2][ab nb*G*2]
 inline long gn_part_floats(const GNShape& s) { return (long)s.nb * s.nchunk * s.groups * 2; }
-
-inline dim3 ew_grid(long n) {
-  long b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
-  return dim3((unsigned)(b < 1 ? 1 : b));
-}
 
 }  // namespace
 
@@ -260,8 +286,8 @@ extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2
   const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
   hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, eps, 0, stats);
-  hipLaunchKernelGGL(gn_apply_kernel, ew_grid((long)nb * hw * s.cgs), dim3(256), 0, st, s, stats, gamma, beta, silu,
-                     (bf16*)y, ldy);
+  const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
+  hipLaunchKernelGGL(gn_apply_kernel, agrid, dim3(threads), 0, st, s, stats, gamma, beta, silu, (bf16*)y, ldy);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -280,9 +306,10 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, stats, gamma, beta, silu,
                      (const bf16*)dy, lddy, ws);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
-  hipLaunchKernelGGL(gn_bwd_apply_kernel, ew_grid((long)nb * hw * s.cgs), dim3(256), 0, st, s, stats, gamma, beta,
-                     silu, (const bf16*)dy, lddy, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1,
-                     (const bf16*)add2, ldadd2);
+  const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, agrid, dim3(threads), 0, st, s, stats, gamma, beta, silu,
+                     (const bf16*)dy, lddy, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1, (const bf16*)add2,
+                     ldadd2);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

@@ -1,0 +1,20 @@
+"""GroupNorm(+SiLU) fwd / bwd timing at the UNet shapes (GPU)."""
+import sys
+import torch
+sys.path.insert(0, ".")
+from depth_completion_amd import ops  # noqa: E402
+from depth_completion_amd.ops import Ctx  # noqa: E402
+dev = torch.device("cuda:0"); ctx = Ctx(dev)
+for nb, hw, c in [(1, 6912, 320), (1, 6912, 640), (1, 1728, 640), (1, 432, 1280), (1, 108, 2560), (8, 6912, 320)]:
+    x = torch.randn(nb * hw, c, device=dev).to(torch.bfloat16)
+    g, b = torch.ones(c, device=dev), torch.zeros(c, device=dev)
+    y = torch.empty_like(x); st = torch.empty(nb, 32, 2, device=dev); dy = torch.randn_like(x); dx = torch.empty_like(x)
+    for name, fn in [("fwd", lambda: ops.groupnorm(ctx, x, nb, hw, c, g, b, 1e-5, True, y, st)),
+                     ("bwd", lambda: ops.groupnorm_bwd(ctx, x, nb, hw, c, g, b, True, st, dy, dx))]:
+        for _ in range(3): fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20): fn()
+        e1.record(); torch.cuda.synchronize()
+        print(f"nb={nb} hw={hw} C={c} {name}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us", flush=True)
