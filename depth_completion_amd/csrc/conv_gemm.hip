@@ -53,8 +53,22 @@ namespace {
 // 16-B buffer stores / loads with the sc1 cache policy (device-coherent hand-off between workgroups);
 // the buffer builtins keep the compiler's vmcnt tracking (an inline-asm load would not)
 constexpr int kSc1 = 16;  // CPol::SC1 on gfx94x/gfx950
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(float* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+// raw buffer resource over [base, base + 2 GiB); the base goes through readfirstlane so the compiler
+// keeps the descriptor in SGPRs (a VGPR descriptor turns every buffer access into a waterfall loop)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  const unsigned long long a = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ws_rsrc(float* base) { return buf_rsrc(base); }
+// 16-B LDS-DMA piece: buffer_load_dwordx4 ... lds.  (The builtin only exists for the device pass; in the
+// host pass of a __global__ template it silently drops the kernel's launch stub, hence the guard.)
+__device__ __forceinline__ void buf_load_lds16(__amdgpu_buffer_rsrc_t r, DC_LDS char* dst, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+#endif
 }
 __device__ __forceinline__ void store_sc1_x4(__amdgpu_buffer_rsrc_t r, long off_f, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(off_f * 4), 0, kSc1);
@@ -190,12 +204,21 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   RowTab rt[AP];
   int a_sw[AP];
   unsigned vmask[AP];
+  int pn[AP], poy[AP], pox[AP];  // !SMALLC: output pixel (frame, y, x) of each piece's row; pn < 0 past M
 #pragma unroll
   for (int j = 0; j < AP; ++j) {
     const int row = tid / CPR + RPI * j;
     a_sw[j] = slot ^ swz<BK>(row);  // logical 16-B chunk this lane fetches (XOR swizzle via the source)
     const long m = m0 + row;
     vmask[j] = 0u;
+    if constexpr (!SMALLC) {
+      const int n = m < M ? (int)(m / hwo) : -1;
+      const int rem = m < M ? (int)(m - (long)n * hwo) : 0;
+      pn[j] = n;
+      poy[j] = rem / p.wout;
+      pox[j] = rem - poy[j] * p.wout;
+      continue;
+    }
     int yp[3] = {0, 0, 0}, xp[3] = {0, 0, 0};
     if (m < M) {
       const int n = (int)(m / hwo);
@@ -239,58 +262,78 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     }
     rt[j] = RowTab{yp[0], yp[1], yp[2], xp[0], xp[1], xp[2]};
   }
-  const bf16* b_src[BP];
-  bool b_ok[BP];
+  const int cch = SMALLC ? 1 : (p.cin / BK);
+  const bf16* zero = (const bf16*)g_zero_line;
+
+  // ---- producer.  !SMALLC: buffer_load ... lds with a per-lane 32-bit voffset that is fixed for a
+  // whole tap (recomputed only when the tap changes) and the channel offset of the chunk in the
+  // scalar soffset, so a chunk costs no address VALU; padding / tails read out of range (offset
+  // >= 2 GiB, zero-filled by the buffer unit).  SMALLC (cin % 64 != 0, first layers) keeps a
+  // per-piece LDS-DMA gather from the zero line.
+  constexpr int kOOB = (int)0x80000000u;
+  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(p.x);
+  const __amdgpu_buffer_rsrc_t ra2 = buf_rsrc(p.x2);
+  const __amdgpu_buffer_rsrc_t rb = buf_rsrc(p.w);
+  int a_off[AP], a_off2[AP], b_off[BP];
 #pragma unroll
   for (int j = 0; j < BP; ++j) {
     const int row = tid / CPR + RPI * j;
     const int co = n0 + row;
-    b_ok[j] = co < p.cout;
-    b_src[j] = p.w + (long)(b_ok[j] ? co : 0) * p.ktot + ((slot ^ swz<BK>(row)) * 8);
+    b_off[j] = co < p.cout ? (co * p.ktot + (slot ^ swz<BK>(row)) * 8) * 2 : kOOB;
   }
-  const int cch = SMALLC ? 1 : (p.cin / BK);
-  const bf16* zero = (const bf16*)g_zero_line;
+  const bool two_src = p.c1 < p.cin;
+  // voffsets of the current tap, recomputed from the pixel coordinates (9 times per conv at most)
+  auto set_tap = [&](int tap) __attribute__((always_inline)) {
+    const int ty = p.kw == 3 ? tap / 3 : 0, tx = p.kw == 3 ? tap - (tap / 3) * 3 : 0;
+#pragma unroll
+    for (int j = 0; j < AP; ++j) {
+      int iy, ix;
+      bool ok;
+      if (p.mode == 0) {
+        iy = poy[j] * p.stride - p.pad + ty;
+        ix = pox[j] * p.stride - p.pad + tx;
+        ok = iy >= 0 && iy < p.hin && ix >= 0 && ix < p.win;
+      } else if (p.mode == 1) {
+        const int vy = poy[j] - p.pad + ty, vx = pox[j] - p.pad + tx;
+        ok = vy >= 0 && vy < p.hout && vx >= 0 && vx < p.wout;
+        iy = ok ? (int)(((long)vy * p.hin) / p.hout) : 0;
+        ix = ok ? (int)(((long)vx * p.win) / p.wout) : 0;
+      } else {
+        const int yy = poy[j] - 1 + ty, xx = pox[j] - 1 + tx;
+        ok = yy >= 0 && !(yy & 1) && (yy >> 1) < p.hin && xx >= 0 && !(xx & 1) && (xx >> 1) < p.win;
+        iy = yy >> 1;
+        ix = xx >> 1;
+      }
+      ok = ok && pn[j] >= 0;
+      const int pix = (pn[j] * p.hin + iy) * p.win + ix;
+      a_off[j] = ok ? (pix * p.ldx + a_sw[j] * 8) * 2 : kOOB;
+      if (two_src) a_off2[j] = ok ? (pix * p.ldx2 + a_sw[j] * 8) * 2 : kOOB;
+    }
+  };
+  // issue cursor: next chunk's tap and channel offset (one division at the start of the range)
+  // (readfirstlane: the integer division runs on the VALU, and a VGPR soffset / branch condition would
+  // be waterfalled)
+  int q_k = kc_begin;
+  int q_tap = SMALLC ? 0 : __builtin_amdgcn_readfirstlane(kc_begin / cch);
+  int q_c = SMALLC ? 0 : __builtin_amdgcn_readfirstlane((kc_begin - q_tap * cch) * BK);
+  if (!SMALLC && nkc > 0) set_tap(q_tap);
 
-  auto issue = [&](int kc, int stage) {
+  auto issue = [&](int stage) __attribute__((always_inline)) {
     DC_LDS char* sbase = (DC_LDS char*)smem + stage * STAGE;
     if (!SMALLC) {
-      // the whole BK-channel chunk sits in one tap and one source (c1 % 64 == 0): uniform scalars;
-      // the tap is dispatched to a compile-time (ky, kx) so the row tables stay in registers
-      const int tap = kc / cch;
-      const int c0 = (kc - tap * cch) * BK;
-      const bool second = c0 >= p.c1;
-      const bf16* base = second ? p.x2 + (c0 - p.c1) : p.x + c0;
-      const int ld = second ? p.ldx2 : p.ldx;
-      auto gather = [&](auto KY, auto KX) {
-        constexpr int ky = decltype(KY)::value, kx = decltype(KX)::value;
-        constexpr int t = ky * 3 + kx;
+      if (q_c >= p.c1) {  // uniform: the chunk comes from the second concat source
 #pragma unroll
-        for (int j = 0; j < AP; ++j) {
-          const int yy = ky == 0 ? rt[j].y0 : (ky == 1 ? rt[j].y1 : rt[j].y2);
-          const int xx = kx == 0 ? rt[j].x0 : (kx == 1 ? rt[j].x1 : rt[j].x2);
-          const bool ok = (vmask[j] >> (p.kw == 3 ? t : 0)) & 1u;
-          const bf16* src = ok ? base + (long)(yy + xx) * ld + a_sw[j] * 8 : zero;
-          __builtin_amdgcn_global_load_lds((const void*)src, sbase + (wid * 64 + 256 * j) * 16, 16, 0, 0);
-        }
-      };
-      using Z = std::integral_constant<int, 0>;
-      using O = std::integral_constant<int, 1>;
-      using T = std::integral_constant<int, 2>;
-      switch (p.kw == 3 ? tap : 0) {
-        case 0: gather(Z{}, Z{}); break;
-        case 1: gather(Z{}, O{}); break;
-        case 2: gather(Z{}, T{}); break;
-        case 3: gather(O{}, Z{}); break;
-        case 4: gather(O{}, O{}); break;
-        case 5: gather(O{}, T{}); break;
-        case 6: gather(T{}, Z{}); break;
-        case 7: gather(T{}, O{}); break;
-        default: gather(T{}, T{}); break;
+        for (int j = 0; j < AP; ++j)
+          buf_load_lds16(ra2, sbase + (wid * 64 + 256 * j) * 16, a_off2[j], (q_c - p.c1) * 2);
+      } else {
+#pragma unroll
+        for (int j = 0; j < AP; ++j)
+          buf_load_lds16(ra, sbase + (wid * 64 + 256 * j) * 16, a_off[j], q_c * 2);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < AP; ++j) {
-        const int k = kc * BK + a_sw[j] * 8;
+        const int k = q_k * BK + a_sw[j] * 8;
         const int tap = k / p.cin;
         const int c = k - tap * p.cin;
         const int ky = tap / p.kw, kx = tap - (tap / p.kw) * p.kw;
@@ -302,9 +345,16 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
       }
     }
 #pragma unroll
-    for (int j = 0; j < BP; ++j) {
-      const void* src = b_ok[j] ? (const void*)(b_src[j] + kc * BK) : (const void*)zero;
-      __builtin_amdgcn_global_load_lds(src, sbase + BM * RB + (wid * 64 + 256 * j) * 16, 16, 0, 0);
+    for (int j = 0; j < BP; ++j)
+      buf_load_lds16(rb, sbase + BM * RB + (wid * 64 + 256 * j) * 16, b_off[j], q_k * BK * 2);
+    ++q_k;
+    if (!SMALLC) {
+      q_c += BK;
+      if (q_c == p.cin) {
+        q_c = 0;
+        ++q_tap;
+        if (q_k < kc_end) set_tap(q_tap);
+      }
     }
   };
 
@@ -314,13 +364,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int s = 0; s < S - 1 && s < nkc; ++s) issue(kc_begin + s, s);
+  for (int s = 0; s < S - 1 && s < nkc; ++s) issue(s);
   for (int i = 0; i < nkc; ++i) {
     wait_chunks<L, S>(min(S - 2, nkc - 1 - i));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (i + S - 1 < nkc) issue(kc_begin + i + S - 1, (i + S - 1) % S);
+    if (i + S - 1 < nkc) issue((i + S - 1) % S);
     const char* sa = smem + (i % S) * STAGE;
     const char* sb = sa + BM * RB;
     bf16x8 af[KS][MI], bfr[KS][NJ];
