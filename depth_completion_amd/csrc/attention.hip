@@ -7,6 +7,8 @@
 // lane-local; P feeds the P.V MFMA straight from the accumulator (O^T = V^T P^T) with V^T fragments
 // from ds_read_b64_tr_b16.  The backward is split into a dK/dV kernel (keys resident per wave,
 // sweeping queries) and a dQ kernel (queries resident, sweeping keys): deterministic, no atomics.
+#include <type_traits>
+
 #include "common.h"
 #include "../../include/dcamd.h"
 
@@ -98,29 +100,132 @@ __device__ __forceinline__ void stage_store(bf16* tile, int stride, const uint4 
   }
 }
 
+// ---------------------------------------------------------------- LDS-DMA tiles (swizzled, unpadded)
+// K / V / Q / dO tiles are [64 rows][64 bf16] = 128-B rows written by buffer_load_dwordx4 ... lds.
+// The 16-B chunk c of row r lives at chunk c ^ tsw(r): conflict-free for the ds_read_b128 fragment
+// reads (32 rows, one chunk per lane group) and for the ds_read_b64_tr_b16 transposed reads (rows
+// k0..k0+3 / +8, 8-B pieces of 32 columns).
+constexpr int kOOB = (int)0x80000000u;  // out-of-range buffer offset: the DMA writes zeros
+constexpr int TILE_B = 64 * 128;
+
+__device__ __forceinline__ int tsw(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int tile_off(int r, int c) { return r * 128 + (((c >> 3) ^ tsw(r)) << 4) + (c & 7) * 2; }
+
+__device__ __forceinline__ bf16x8 row_frag(const char* tile, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(tile + row * 128 + ((chunk ^ tsw(row)) << 4));
+}
+
+// byte offsets of a lane's two tr_b16 reads for trans_frag_sw(key_base, col_base): loop-invariant,
+// so kernels precompute them once (the swizzle arithmetic would otherwise be VALU in every tile)
+struct TrOff {
+  int lo, hi;
+};
+__device__ __forceinline__ TrOff tr_off(int key_base, int col_base, int lane) {
+  const int g = lane >> 4, i = lane & 15, hh = lane >> 5;
+  const int col = col_base + 16 * (g & 1) + 4 * (i & 3);
+  const int k0 = key_base + 4 * hh + (i >> 2);
+  return TrOff{tile_off(k0, col), tile_off(k0 + 8, col)};
+}
+__device__ __forceinline__ bf16x8 trans_frag_at(const char* tile, TrOff o) {
+  bf16x4 lo = tr_read(reinterpret_cast<const bf16*>(tile + o.lo));
+  bf16x4 hi = tr_read(reinterpret_cast<const bf16*>(tile + o.hi));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+__device__ __forceinline__ int row_off(int row, int chunk) { return row * 128 + ((chunk ^ tsw(row)) << 4); }
+
+// transposed A-operand fragment from a swizzled tile (same element order as trans_frag)
+__device__ __forceinline__ bf16x8 trans_frag_sw(const char* tile, int key_base, int col_base, int lane) {
+  const int g = lane >> 4, i = lane & 15, hh = lane >> 5;
+  const int qq = i >> 2, pp = i & 3;
+  const int col = col_base + 16 * (g & 1) + 4 * pp;
+  const int k0 = key_base + 4 * hh + qq;
+  bf16x4 lo = tr_read(reinterpret_cast<const bf16*>(tile + tile_off(k0, col)));
+  bf16x4 hi = tr_read(reinterpret_cast<const bf16*>(tile + tile_off(k0 + 8, col)));
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base) {
+  const unsigned long long a = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+// (the builtin exists only in the device pass; unguarded it silently drops the host launch stub)
+__device__ __forceinline__ void buf_load_lds16(__amdgpu_buffer_rsrc_t r, DC_LDS char* dst, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+#endif
+}
+__device__ __forceinline__ void buf_load_lds4(__amdgpu_buffer_rsrc_t r, DC_LDS char* dst, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 4, voff, soff, 0, 0);
+#endif
+}
+
+// one 64-row tile by the NT threads of a split: 512 pieces of 16 B, piece p = lt + NT i, one LDS-DMA
+// wave-instruction per 64 consecutive pieces; the source offset of each piece is fixed, the tile's
+// first row rides in soffset, rows >= T read zero
+template <int NT>
+struct TileDma {
+  static constexpr int PPT = (512 + NT - 1) / NT;
+  static constexpr int MIN_INSTR = 512 / NT;  // instructions per tile issued by every wave (>=)
+  int voff[PPT], prow[PPT];
+  __device__ __forceinline__ void init(int lt, int ld) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int p = lt + NT * i, r = p >> 3;
+      prow[i] = r;
+      voff[i] = r * ld * 2 + (((p & 7) ^ tsw(r)) << 4);
+    }
+  }
+  // (wave index and soffset go through readfirstlane: derived from threadIdx, the compiler would
+  // otherwise treat them as divergent and waterfall every buffer access)
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* tile, int r0, int T, int ld, int lt) {
+    const int wv = __builtin_amdgcn_readfirstlane(lt >> 6);
+    const int soff = __builtin_amdgcn_readfirstlane(r0 * ld * 2);
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int first = 64 * wv + NT * i;
+      if (first < 512) buf_load_lds16(rs, (DC_LDS char*)tile + first * 16, r0 + prow[i] < T ? voff[i] : kOOB, soff);
+    }
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // ------------------------------------------------------------------------------ forward
-// KS key-splits per block: waves 4p..4p+3 sweep the p-th contiguous range of key tiles for the same
-// 128 queries (KS x 4 waves per CU hide MFMA / softmax / LDS latency at small T x heads), then the
-// partial (m, l, O) are merged through LDS in a fixed order (deterministic).
+// KS key-splits per block: waves QW p .. QW p + QW - 1 sweep the p-th contiguous range of key tiles
+// for the same 32 QW queries, then the partial (m, l, O) are merged through LDS in a fixed order.
+// K / V tiles stream through an S-deep LDS-DMA ring per split (one barrier per tile).
+constexpr int FWD_S = 3;
 template <int QW, int KS>
 struct FwdLds {
-  static constexpr int K_BYTES = KS * 2 * 64 * KSTR * 2;
-  static constexpr int V_BYTES = KS * 2 * 64 * VSTR * 2;
+  static constexpr int STAGE = 2 * TILE_B;                      // K + V
+  static constexpr int RING = KS * FWD_S * STAGE;
   static constexpr int RED = (KS - 1) * QW * 34 * 64 * 4;
-  static constexpr int BYTES = (K_BYTES + V_BYTES > RED) ? K_BYTES + V_BYTES : RED;
+  static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
 template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(const bf16* qkv, int ld, int T, int heads, bf16* o,
-                                                            int ldo, float* lse) {
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(
+    const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse) {
   __shared__ __attribute__((aligned(16))) char smem[FwdLds<QW, KS>::BYTES];
-  constexpr int NT = 64 * QW;  // threads per key/query split
-  constexpr int PPT = ppt<NT>();
+  constexpr int NT = 64 * QW;
+  constexpr int S = FWD_S;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
   const int lt = threadIdx.x - part * NT;
-  bf16* ks = reinterpret_cast<bf16*>(smem) + part * 2 * 64 * KSTR;
-  bf16* vs = reinterpret_cast<bf16*>(smem + FwdLds<QW, KS>::K_BYTES) + part * 2 * 64 * VSTR;
+  char* ring = smem + part * S * FwdLds<QW, KS>::STAGE;
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
@@ -141,98 +246,104 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   const int per = (ntiles + KS - 1) / KS;
   const int tb = part * per;
   const int mine = max(0, min(ntiles, tb + per) - tb);
-  // two register stages: tile i+2 is fetched while tile i is computed and tile i+1 is written to LDS
-  uint4 ra[2][PPT], rb[2][PPT];
-  if (mine > 0) {
-    stage_load<NT>(base, ld, tb * 64, T, C + h * 64, ra[0], lt);
-    stage_load<NT>(base, ld, tb * 64, T, 2 * C + h * 64, ra[1], lt);
-    stage_store<NT>(ks, KSTR, ra[0], 1.0f, lt);
-    stage_store<NT>(vs, VSTR, ra[1], 1.0f, lt);
-  }
-  if (mine > 1) {
-    stage_load<NT>(base, ld, (tb + 1) * 64, T, C + h * 64, rb[0], lt);
-    stage_load<NT>(base, ld, (tb + 1) * 64, T, 2 * C + h * 64, rb[1], lt);
-  }
-  __syncthreads();
-  auto body = [&](int i, uint4 (&held)[2][PPT], uint4 (&fresh)[2][PPT]) {
-    const int kt = tb + i;
-    const int cur = i & 1;
-    if (i + 2 < mine) {
-      stage_load<NT>(base, ld, (kt + 2) * 64, T, C + h * 64, fresh[0], lt);
-      stage_load<NT>(base, ld, (kt + 2) * 64, T, 2 * C + h * 64, fresh[1], lt);
-    }
-      if (i < mine) {
-        const bf16* kt_s = ks + cur * 64 * KSTR;
-        const bf16* vt_s = vs + cur * 64 * VSTR;
-        f32x16 sacc[2];
-  #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
-  #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-            sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[b], 0, 0, 0);
-          }
-        }
-        // online softmax in raw score units; exp2 with log2(e) folded into one FMA per score;
-        // keys beyond T exist only in the last tile; O is rescaled only when some row max grew
-        if ((kt + 1) * 64 > T) {
-  #pragma unroll
-          for (int b = 0; b < 2; ++b)
-  #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-              if (key >= T) sacc[b][r] = -INFINITY;
-            }
-        }
-        float mx = -INFINITY;
-  #pragma unroll
-        for (int b = 0; b < 2; ++b)
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[b][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m, mx);
-        const float ml = mnew * LOG2E;
-        float ps = 0.0f;
-  #pragma unroll
-        for (int b = 0; b < 2; ++b)
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
-            sacc[b][r] = pv;
-            ps += pv;
-          }
-        if (__any(mnew > m)) {
-          const float alpha = fast_exp2((m - mnew) * LOG2E);
-          l *= alpha;
-  #pragma unroll
-          for (int db = 0; db < 2; ++db)
-  #pragma unroll
-            for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-        }
-        l += ps;
-        m = mnew;
-  #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
-  #pragma unroll
-          for (int db = 0; db < 2; ++db) {
-            const bf16x8 vf = trans_frag(vt_s, VSTR, 16 * s, 32 * db, lane);
-            oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, oacc[db], 0, 0, 0);
-          }
-        }
-      }
-    if (i + 1 < mine) {
-      stage_store<NT>(ks + (cur ^ 1) * 64 * KSTR, KSTR, held[0], 1.0f, lt);
-      stage_store<NT>(vs + (cur ^ 1) * 64 * VSTR, VSTR, held[1], 1.0f, lt);
-    }
-    __syncthreads();
+  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
+  const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
+  TileDma<NT> dma;
+  dma.init(lt, ld);
+  auto issue = [&](int i) __attribute__((always_inline)) {
+    char* st = ring + (i % S) * FwdLds<QW, KS>::STAGE;
+    dma.issue(rk, st, (tb + i) * 64, T, ld, lt);
+    dma.issue(rv, st + TILE_B, (tb + i) * 64, T, ld, lt);
   };
-  for (int i = 0; i < per; i += 2) {
-    body(i, rb, ra);
-    if (i + 1 < per) body(i + 1, ra, rb);
+  constexpr int PER_TILE = 2 * TileDma<NT>::MIN_INSTR;  // LDS-DMA instructions per stage, every wave
+  int koff[2][4];
+  TrOff voff[4][2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) koff[b][s] = row_off(32 * b + (lane & 31), 2 * s + hh);
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int db = 0; db < 2; ++db) voff[s][db] = tr_off(16 * s, 32 * db, lane);
+  for (int i = 0; i < S - 1 && i < mine; ++i) issue(i);
+  // the ring stage is a compile-time constant in each copy of the body (ds_read immediate offsets)
+  auto step = [&](int i, auto STC) __attribute__((always_inline)) {
+    constexpr int ST = decltype(STC)::value;
+    if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();  // S = 3: at most one younger tile in flight
+    else vm_wait_n<0>();
+    __syncthreads();
+    if (i + S - 1 < mine) issue(i + S - 1);
+    if (i < mine) {
+      const int kt = tb + i;
+      const char* kt_s = ring + ST * FwdLds<QW, KS>::STAGE;
+      const char* vt_s = kt_s + TILE_B;
+      f32x16 sacc[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              *reinterpret_cast<const bf16x8*>(kt_s + koff[b][s]), qf[s], sacc[b], 0, 0, 0);
+      }
+      // online softmax in raw score units; exp2 with log2(e) folded into one FMA per score;
+      // keys beyond T exist only in the last tile; O is rescaled only when some row max grew
+      if ((kt + 1) * 64 > T) {
+        asm volatile("" ::: "memory");  // keep this a branch: if-converted it costs ~60 VALU per tile
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= T) sacc[b][r] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[b][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(m, mx);
+      const float ml = mnew * LOG2E;
+      float ps = 0.0f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+          sacc[b][r] = pv;
+          ps += pv;
+        }
+      if (__any(mnew > m)) {
+        const float alpha = fast_exp2((m - mnew) * LOG2E);
+        l *= alpha;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+      }
+      l += ps;
+      m = mnew;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(vt_s, voff[s][db]), pf, oacc[db], 0, 0, 0);
+      }
+    }
+  };
+  static_assert(S == 3, "the unrolled ring below assumes three stages");
+  for (int i = 0; i < per; i += 3) {
+    step(i, std::integral_constant<int, 0>{});
+    if (i + 1 < per) step(i + 1, std::integral_constant<int, 1>{});
+    if (i + 2 < per) step(i + 2, std::integral_constant<int, 2>{});
   }
+  vm_wait_n<0>();
+  __syncthreads();
   if constexpr (KS > 1) {
     // merge the key-split partials: parts 1.. publish (m, l, O) per lane, part 0 folds them in order
     float* red = reinterpret_cast<float*>(smem);
@@ -249,7 +360,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
     if (part > 0) return;
 #pragma unroll
     for (int p = 1; p < KS; ++p) {
-      const float* src = red + ((p - 1) * 4 + wid) * 34 * 64 + lane;
+      const float* src = red + ((p - 1) * QW + wid) * 34 * 64 + lane;
       const float mp = src[0], lp = src[64];
       const float mn = fmaxf(m, mp);
       const float a0 = fast_exp2((m - mn) * LOG2E), a1 = fast_exp2((mp - mn) * LOG2E);
