@@ -411,31 +411,31 @@ __global__ void attn_delta_kernel(const bf16* o, int ldo, const bf16* dout, int 
   delta[(n * heads + h) * T + q] = s;
 }
 
-// dK/dV: 128 keys per block resident in registers (32 per wave); KS query-splits per block (waves
-// 4p..4p+3 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a fixed order.
+// dK/dV: 32 QW keys per block resident in registers (32 per wave); KS query-splits per block (waves
+// QW p .. QW p + QW - 1 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a
+// fixed order.  Q / dO tiles (+ lse / delta rows) stream through an LDS-DMA ring; Q is not pre-scaled
+// (the 1/8 softmax scale is folded into the exp argument and into dK at the end).
+constexpr int BWD_S = 3;
 template <int QW, int KS>
 struct DkdvLds {
-  static constexpr int TILE = 64 * KSTR * 2;
-  static constexpr int MAIN = KS * 2 * 2 * TILE + KS * 2 * 2 * 64 * 4;
+  static constexpr int STAGE = 2 * TILE_B + 2 * 64 * 4;     // Q, dO, lse, delta
+  static constexpr int RING = KS * BWD_S * STAGE;
   static constexpr int RED = (KS - 1) * QW * 64 * 64 * 4;
-  static constexpr int BYTES = MAIN > RED ? MAIN : RED;
+  static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
 template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
-                                                                 const float* lse, const float* delta, int T,
-                                                                 int heads, bf16* dqkv, int ldd) {
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(
+    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
+    bf16* dqkv, int ldd) {
   __shared__ __attribute__((aligned(16))) char smem[DkdvLds<QW, KS>::BYTES];
-  constexpr int NT = 64 * QW;  // threads per key/query split
-  constexpr int PPT = ppt<NT>();
+  constexpr int NT = 64 * QW;
+  constexpr int S = BWD_S;
+  constexpr int STG = DkdvLds<QW, KS>::STAGE;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
   const int lt = threadIdx.x - part * NT;
-  constexpr int TILE = DkdvLds<QW, KS>::TILE;
-  bf16* qs = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE);       // [2 stages][64 * KSTR]
-  bf16* ds_ = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE + 2 * TILE);
-  float* ls = reinterpret_cast<float*>(smem + KS * 2 * 2 * TILE) + part * 2 * 2 * 64;  // [2][64]
-  float* dl = ls + 2 * 64;
+  char* ring = smem + part * S * STG;
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
@@ -460,89 +460,96 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   const int per = (ntiles + KS - 1) / KS;
   const int tb = part * per;
   const int mine = max(0, min(ntiles, tb + per) - tb);
-  // two register stages (Q / dO pieces + lse / delta): tile i+2 is fetched while tile i is computed
-  struct Stage {
-    uint4 q[PPT], d[PPT];
-    float l, dl;
-  };
-  Stage sa, sb;
-  auto load_tile = [&](int qt, Stage& r) {
-    stage_load<NT>(base, ld, qt * 64, T, h * 64, r.q, lt);
-    stage_load<NT>(dob, lddo, qt * 64, T, h * 64, r.d, lt);
-    if (lt < 64) {
-      const int q = qt * 64 + lt;
-      r.l = q < T ? lse_b[q] * LOG2E : INFINITY;  // consumed as exp2(S log2e - lse log2e)
-      r.dl = q < T ? del_b[q] : 0.0f;
+  const __amdgpu_buffer_rsrc_t rq = buf_rsrc(base + h * 64);
+  const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dob + h * 64);
+  const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lse_b);
+  const __amdgpu_buffer_rsrc_t rdl = buf_rsrc(del_b);
+  TileDma<NT> dq_dma, do_dma;
+  dq_dma.init(lt, ld);
+  do_dma.init(lt, lddo);
+  const int wv = __builtin_amdgcn_readfirstlane(lt >> 6);
+  auto issue = [&](int i) __attribute__((always_inline)) {
+    char* st = ring + (i % S) * STG;
+    const int r0 = (tb + i) * 64;
+    dq_dma.issue(rq, st, r0, T, ld, lt);
+    do_dma.issue(rd, st + TILE_B, r0, T, lddo, lt);
+    if (wv == 0) {  // lse / delta rows of the tile: 64 x 4 B each (rows >= T read 0; their dO rows are 0 too)
+      const int soff = __builtin_amdgcn_readfirstlane(r0 * 4);
+      buf_load_lds4(rl, (DC_LDS char*)st + 2 * TILE_B, r0 + lane < T ? lane * 4 : kOOB, soff);
+      buf_load_lds4(rdl, (DC_LDS char*)st + 2 * TILE_B + 256, r0 + lane < T ? lane * 4 : kOOB, soff);
     }
   };
-  auto store_tile = [&](int st, const Stage& r) {
-    stage_store<NT>(qs + st * 64 * KSTR, KSTR, r.q, 0.125f, lt);
-    stage_store<NT>(ds_ + st * 64 * KSTR, KSTR, r.d, 1.0f, lt);
-    if (lt < 64) {
-      ls[st * 64 + lt] = r.l;
-      dl[st * 64 + lt] = r.dl;
-    }
-  };
-  if (mine > 0) {
-    load_tile(tb, sa);
-    store_tile(0, sa);
+  // per-lane LDS offsets (loop-invariant)
+  int qoff[2][4];
+  TrOff toff[2][2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qoff[qb][s] = row_off(32 * qb + (lane & 31), 2 * s + hh);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int db = 0; db < 2; ++db) toff[qb][s2][db] = tr_off(32 * qb + 16 * s2, 32 * db, lane);
   }
-  if (mine > 1) load_tile(tb + 1, sb);
-  __syncthreads();
-  auto body = [&](int i, Stage& held, Stage& fresh) {
-    const int qt = tb + i;
-    const int cur = i & 1;
-    if (i + 2 < mine) load_tile(qt + 2, fresh);
-      if (i < mine) {
-        const bf16* qt_s = qs + cur * 64 * KSTR;
-        const bf16* dt_s = ds_ + cur * 64 * KSTR;
-  #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          // S and dP from zero accumulators; lse (pre-scaled by log2 e) and delta are read 4 rows per
-          // ds_read_b128: accumulator element r holds query row 32 qb + 8 (r >> 2) + 4 hh + (r & 3)
-          f32x16 sp = {}, dp = {};
-  #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const bf16x8 qa =
-                *reinterpret_cast<const bf16x8*>(qt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-            sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sp, 0, 0, 0);
-            const bf16x8 da =
-                *reinterpret_cast<const bf16x8*>(dt_s + (32 * qb + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, vf[s], dp, 0, 0, 0);
+  constexpr int PER_TILE = 2 * TileDma<NT>::MIN_INSTR;
+  constexpr float L8 = LOG2E * 0.125f;
+  for (int i = 0; i < S - 1 && i < mine; ++i) issue(i);
+  auto step = [&](int i, auto STC) __attribute__((always_inline)) {
+    constexpr int ST = decltype(STC)::value;
+    if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();  // (wave 0 also has the lse/delta pieces: conservative)
+    else vm_wait_n<0>();
+    __syncthreads();
+    if (i + S - 1 < mine) issue(i + S - 1);
+    if (i < mine) {
+      const char* qt_s = ring + ST * STG;
+      const char* dt_s = qt_s + TILE_B;
+      const float* ls = reinterpret_cast<const float*>(qt_s + 2 * TILE_B);
+      const float* dl = ls + 64;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        // S and dP from zero accumulators; accumulator element r holds query row
+        // 32 qb + 8 (r >> 2) + 4 hh + (r & 3): lse / delta are read 4 rows per ds_read_b128
+        f32x16 sp = {}, dp = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(qt_s + qoff[qb][s]), kf[s],
+                                                       sp, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(dt_s + qoff[qb][s]), vf[s],
+                                                       dp, 0, 0, 0);
+        }
+        // P = exp2(S_raw log2e / 8 - lse log2e); dS = P * (dP - delta)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + 32 * qb + 8 * g + 4 * hh);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + 32 * qb + 8 * g + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pv = fast_exp2(fmaf(sp[4 * g + e], L8, -l4[e] * LOG2E));
+            sp[4 * g + e] = pv;
+            dp[4 * g + e] = pv * (dp[4 * g + e] - d4[e]);
           }
-          // P = exp2(S log2e - lse log2e); dS = P * (dP - delta)
-  #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + cur * 64 + 32 * qb + 8 * g + 4 * hh);
-            const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + cur * 64 + 32 * qb + 8 * g + 4 * hh);
-  #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float pv = fast_exp2(fmaf(sp[4 * g + e], LOG2E, -l4[e]));
-              sp[4 * g + e] = pv;
-              dp[4 * g + e] = pv * (dp[4 * g + e] - d4[e]);
-            }
-          }
-  #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const bf16x8 pf = acc_to_frag(sp, s2);
-            const bf16x8 sf = acc_to_frag(dp, s2);
-  #pragma unroll
-            for (int db = 0; db < 2; ++db) {
-              const bf16x8 doT = trans_frag(dt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
-              dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(doT, pf, dv[db], 0, 0, 0);
-              const bf16x8 qT = trans_frag(qt_s, KSTR, 32 * qb + 16 * s2, 32 * db, lane);
-              dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qT, sf, dk[db], 0, 0, 0);
-            }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 pf = acc_to_frag(sp, s2);
+          const bf16x8 sf = acc_to_frag(dp, s2);
+#pragma unroll
+          for (int db = 0; db < 2; ++db) {
+            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(dt_s, toff[qb][s2][db]), pf, dv[db], 0, 0, 0);
+            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(qt_s, toff[qb][s2][db]), sf, dk[db], 0, 0, 0);
           }
         }
       }
-    if (i + 1 < mine) store_tile(cur ^ 1, held);
-    __syncthreads();
+    }
   };
-  for (int i = 0; i < per; i += 2) {
-    body(i, sb, sa);
-    if (i + 1 < per) body(i + 1, sa, sb);
+  static_assert(S == 3, "the unrolled ring below assumes three stages");
+  for (int i = 0; i < per; i += 3) {
+    step(i, std::integral_constant<int, 0>{});
+    if (i + 1 < per) step(i + 1, std::integral_constant<int, 1>{});
+    if (i + 2 < per) step(i + 2, std::integral_constant<int, 2>{});
   }
+  vm_wait_n<0>();
+  __syncthreads();
   if constexpr (KS > 1) {
     float* red = reinterpret_cast<float*>(smem);
     if (part > 0) {
@@ -559,7 +566,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
     if (part > 0) return;
 #pragma unroll
     for (int p = 1; p < KS; ++p) {
-      const float* src = red + ((p - 1) * 4 + wid) * 64 * 64 + lane;
+      const float* src = red + ((p - 1) * QW + wid) * 64 * 64 + lane;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -578,7 +585,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
         bf16x4 a, b;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          a[e] = (bf16)dk[db][4 * g2 + e];
+          a[e] = (bf16)(dk[db][4 * g2 + e] * 0.125f);  // dK = dS^T (Q / 8)
           b[e] = (bf16)dv[db][4 * g2 + e];
         }
         const int d = 32 * db + 8 * g2 + 4 * hh;
@@ -588,28 +595,28 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   }
 }
 
-// dQ: 128 queries per block resident; KS key-splits per block, partial dQ folded through LDS.
+// dQ: 32 QW queries per block resident; KS key-splits per block, partial dQ folded through LDS.
+// K / V tiles stream through the same LDS-DMA ring as the forward.
 template <int QW, int KS>
 struct DqLds {
-  static constexpr int TILE = 64 * KSTR * 2;
-  static constexpr int MAIN = KS * 2 * 2 * TILE;
+  static constexpr int STAGE = 2 * TILE_B;
+  static constexpr int RING = KS * BWD_S * STAGE;
   static constexpr int RED = (KS - 1) * QW * 32 * 64 * 4;
-  static constexpr int BYTES = MAIN > RED ? MAIN : RED;
+  static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
 template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(const bf16* qkv, int ld, const bf16* dout, int lddo,
-                                                               const float* lse, const float* delta, int T, int heads,
-                                                               bf16* dqkv, int ldd) {
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(
+    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
+    bf16* dqkv, int ldd) {
   __shared__ __attribute__((aligned(16))) char smem[DqLds<QW, KS>::BYTES];
-  constexpr int NT = 64 * QW;  // threads per key/query split
-  constexpr int PPT = ppt<NT>();
+  constexpr int NT = 64 * QW;
+  constexpr int S = BWD_S;
+  constexpr int STG = DqLds<QW, KS>::STAGE;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
   const int lt = threadIdx.x - part * NT;
-  constexpr int TILE = DqLds<QW, KS>::TILE;
-  bf16* ks = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE);
-  bf16* vs = reinterpret_cast<bf16*>(smem + part * 2 * 2 * TILE + 2 * TILE);
+  char* ring = smem + part * S * STG;
   const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
@@ -632,72 +639,77 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   const int per = (ntiles + KS - 1) / KS;
   const int tb = part * per;
   const int mine = max(0, min(ntiles, tb + per) - tb);
-  // two register stages: tile i+2 is fetched while tile i is computed and tile i+1 is written to LDS
-  uint4 ra[2][PPT], rb[2][PPT];
-  if (mine > 0) {
-    stage_load<NT>(base, ld, tb * 64, T, C + h * 64, ra[0], lt);
-    stage_load<NT>(base, ld, tb * 64, T, 2 * C + h * 64, ra[1], lt);
-    stage_store<NT>(ks, KSTR, ra[0], 1.0f, lt);
-    stage_store<NT>(vs, KSTR, ra[1], 1.0f, lt);
+  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
+  const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
+  TileDma<NT> dma;
+  dma.init(lt, ld);
+  auto issue = [&](int i) __attribute__((always_inline)) {
+    char* st = ring + (i % S) * STG;
+    dma.issue(rk, st, (tb + i) * 64, T, ld, lt);
+    dma.issue(rv, st + TILE_B, (tb + i) * 64, T, ld, lt);
+  };
+  int koff[2][4];
+  TrOff toff[2][2][2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) koff[b][s] = row_off(32 * b + (lane & 31), 2 * s + hh);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int db = 0; db < 2; ++db) toff[b][s2][db] = tr_off(32 * b + 16 * s2, 32 * db, lane);
   }
-  if (mine > 1) {
-    stage_load<NT>(base, ld, (tb + 1) * 64, T, C + h * 64, rb[0], lt);
-    stage_load<NT>(base, ld, (tb + 1) * 64, T, 2 * C + h * 64, rb[1], lt);
-  }
-  __syncthreads();
-  auto body = [&](int i, uint4 (&held)[2][PPT], uint4 (&fresh)[2][PPT]) {
-    const int kt = tb + i;
-    const int cur = i & 1;
-    if (i + 2 < mine) {
-      stage_load<NT>(base, ld, (kt + 2) * 64, T, C + h * 64, fresh[0], lt);
-      stage_load<NT>(base, ld, (kt + 2) * 64, T, 2 * C + h * 64, fresh[1], lt);
-    }
-      if (i < mine) {
-        const bf16* kt_s = ks + cur * 64 * KSTR;
-        const bf16* vt_s = vs + cur * 64 * KSTR;
-  #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          f32x16 sp, dp;
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) { sp[r] = 0.0f; dp[r] = 0.0f; }
-  #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const bf16x8 ka = *reinterpret_cast<const bf16x8*>(kt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-            sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sp, 0, 0, 0);
-            const bf16x8 va = *reinterpret_cast<const bf16x8*>(vt_s + (32 * b + (lane & 31)) * KSTR + 16 * s + 8 * hh);
-            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, df[s], dp, 0, 0, 0);
-          }
-  #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float pv = fast_exp2(fmaf(sp[r], LOG2E, -my_lse));
-            sp[r] = pv * (dp[r] - my_del);  // dS^T
-          }
-          if ((kt + 1) * 64 > T) {  // keys beyond T exist only in the last tile
-  #pragma unroll
-            for (int r = 0; r < 16; ++r)
-              if (kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) sp[r] = 0.0f;
-          }
-  #pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) {
-            const bf16x8 sf = acc_to_frag(sp, s2);
-  #pragma unroll
-            for (int db = 0; db < 2; ++db) {
-              const bf16x8 kT = trans_frag(kt_s, KSTR, 32 * b + 16 * s2, 32 * db, lane);
-              dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kT, sf, dq[db], 0, 0, 0);
-            }
-          }
+  constexpr int PER_TILE = 2 * TileDma<NT>::MIN_INSTR;
+  for (int i = 0; i < S - 1 && i < mine; ++i) issue(i);
+  auto step = [&](int i, auto STC) __attribute__((always_inline)) {
+    constexpr int ST = decltype(STC)::value;
+    if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();
+    else vm_wait_n<0>();
+    __syncthreads();
+    if (i + S - 1 < mine) issue(i + S - 1);
+    if (i < mine) {
+      const int kt = tb + i;
+      const char* kt_s = ring + ST * STG;
+      const char* vt_s = kt_s + TILE_B;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f32x16 sp = {}, dp = {};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(kt_s + koff[b][s]), qf[s], sp,
+                                                       0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(vt_s + koff[b][s]), df[s], dp,
+                                                       0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(fmaf(sp[r], LOG2E, -my_lse));
+          sp[r] = pv * (dp[r] - my_del);  // dS^T
+        }
+        if ((kt + 1) * 64 > T) {  // keys beyond T exist only in the last tile
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) sp[r] = 0.0f;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const bf16x8 sf = acc_to_frag(sp, s2);
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(kt_s, toff[b][s2][db]), sf, dq[db], 0, 0, 0);
         }
       }
-    if (i + 1 < mine) {
-      stage_store<NT>(ks + (cur ^ 1) * 64 * KSTR, KSTR, held[0], 1.0f, lt);
-      stage_store<NT>(vs + (cur ^ 1) * 64 * KSTR, KSTR, held[1], 1.0f, lt);
     }
-    __syncthreads();
   };
-  for (int i = 0; i < per; i += 2) {
-    body(i, rb, ra);
-    if (i + 1 < per) body(i + 1, ra, rb);
+  static_assert(S == 3, "the unrolled ring below assumes three stages");
+  for (int i = 0; i < per; i += 3) {
+    step(i, std::integral_constant<int, 0>{});
+    if (i + 1 < per) step(i + 1, std::integral_constant<int, 1>{});
+    if (i + 2 < per) step(i + 2, std::integral_constant<int, 2>{});
   }
+  vm_wait_n<0>();
+  __syncthreads();
   if constexpr (KS > 1) {
     float* red = reinterpret_cast<float*>(smem);
     if (part > 0) {
@@ -711,7 +723,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
     if (part > 0) return;
 #pragma unroll
     for (int p = 1; p < KS; ++p) {
-      const float* src = red + ((p - 1) * 4 + wid) * 32 * 64 + lane;
+      const float* src = red + ((p - 1) * QW + wid) * 32 * 64 + lane;
 #pragma unroll
       for (int db = 0; db < 2; ++db)
 #pragma unroll
