@@ -194,7 +194,7 @@ def main():
     achieved = conv_flops_ / (conv_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                "kernel": "dc_conv_gemm = conv_gemm_kernel (+ splitk_reduce_kernel when split), implicit-GEMM conv/linear",
+                "kernel": "dc_conv_gemm = conv_gemm_kernel (split-K partials reduced in-kernel by the last block), implicit-GEMM conv/linear",
                 "launches_per_step": n_launch, "avg_launch_ms": round(avg_ms, 5),
                 "algorithmic_gflop_per_step": round(conv_flops_ / 1e9, 1)}
     # whole-frame roofline: SURVEY §8(d) canonical 190.4 TFLOP per 768x576 frame (50 guided steps)

@@ -230,11 +230,13 @@ def test_attention_fwd_bwd(ctx, n, t, heads, cfg, monkeypatch):
     assert rel(dq.view(n, t, 3 * C), qkv.grad) < 2e-2
 
 
-def test_cross_attention_fold(ctx):
-    """Folded 2-key cross-attention == LN2 + attn2 (2-token context) + residual."""
+@pytest.mark.parametrize("C,heads", [(320, 5), (640, 10), (1280, 20)])
+def test_cross_attention_fold(ctx, C, heads):
+    """Folded 2-key cross-attention == LN2 + attn2 (2-token context) + residual; the three UNet widths
+    (U and D staged together in LDS at 320 / 640, one after the other at 1280 x 20 heads)."""
     from depth_completion_amd import ops
     from depth_completion_amd.weights import fold_cross_attention
-    rows, C, heads, cross = 257, 320, 5, 1024
+    rows, cross = 257, 1024
     g = torch.Generator().manual_seed(32)
     sd = {"to_q.weight": torch.randn(C, C, generator=g) / math.sqrt(C),
           "to_k.weight": torch.randn(C, cross, generator=g) / math.sqrt(cross),
