@@ -182,16 +182,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   const long M = (long)p.nb * hwo;
   const int tiles_n = (p.cout + BN - 1) / BN;
 
-  // bijective XCD-aware remap: blocks sharing an XCD (b % 8) get a contiguous tile range
-  const int nblk = gridDim.x, bid = blockIdx.x;
+  // bijective XCD-aware remap over the whole (tile, split) grid: workgroups are dealt round-robin to
+  // the 8 XCDs by linear id, so XCD x = id % 8 gets the contiguous work range x * total / 8 ... in
+  // split-major order -- with K split 8 ways each XCD streams one K slice of A and W through its own L2
+  // (each byte fetched from HBM once); unsplit, each XCD gets a contiguous run of row tiles.
+  const int tiles = gridDim.x, nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
   const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  const int lb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int wk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int split = wk / tiles, lb = wk - split * tiles;
   const int tm = lb / tiles_n, tn = lb - tm * tiles_n;
   const long m0 = (long)tm * BM;
   const int n0 = tn * BN;
 
   const int nk = p.ktot / BK;
-  const int kc_begin = blockIdx.y * p.kps;
+  const int kc_begin = split * p.kps;
   const int kc_end = min(nk, kc_begin + p.kps);
   const int nkc = max(0, kc_end - kc_begin);
 
@@ -411,7 +415,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     // (MI355X_MICROARCH.md hand-off table, row 1) and runs the normal epilogue.
     constexpr int TILE_F = BM * BN;
     const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
-    const long slab = ((long)blockIdx.y * gridDim.x + lb) * TILE_F + wid * (WM * WN) + lane * 4;
+    const long slab = ((long)split * gridDim.x + lb) * TILE_F + wid * (WM * WN) + lane * 4;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll

@@ -87,10 +87,21 @@ __global__ void gn_finalize_kernel(GNShape s, const float* part, float eps, int 
     const int g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (g >= s.groups) return;
     double ta = 0.0, tb = 0.0;
-    for (int k = lane; k < s.nchunk; k += 64) {
-      const float* src = part + (((long)n * s.nchunk + k) * s.groups + g) * 2;
-      ta += src[0];
-      tb += src[1];
+    // up to 8 chunk partials per lane in flight at once (a loop-carried chain of loads would pay one
+    // memory round trip per 64 chunks); summation order per lane unchanged: k = lane, lane + 64, ...
+    for (int k0 = lane; k0 < s.nchunk; k0 += 512) {
+      float2 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + 64 * j;
+        v[j] = k < s.nchunk ? *reinterpret_cast<const float2*>(part + (((long)n * s.nchunk + k) * s.groups + g) * 2)
+                            : float2{0.f, 0.f};
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ta += v[j].x;
+        tb += v[j].y;
+      }
     }
     for (int o = 32; o >= 1; o >>= 1) {
       ta += __shfl_xor(ta, o, 64);

@@ -178,6 +178,32 @@ def test_groupnorm_fwd_bwd(ctx, c, silu, two):
     assert rel(nchw(dx, n, h, w), x.grad + gy) < 2e-2
 
 
+@pytest.mark.parametrize("n,h,w,c", [(1, 72, 96, 320), (3, 24, 32, 640), (8, 18, 24, 1280), (1, 1, 5, 64)])
+def test_groupnorm_many_chunks(ctx, n, h, w, c):
+    """GroupNorm where the stats pass spans many blocks (the last-arriving block folds every chunk
+    partial): statistics against torch fp32, and repeated calls bit-identical (counter reset)."""
+    from depth_completion_amd import ops
+    x = (rnd(n, c, h, w, seed=40) * 1.5 - 0.3).to(torch.bfloat16).float()
+    gamma = (1 + 0.1 * rnd(c, seed=41)).to(torch.bfloat16).float()
+    beta = (0.1 * rnd(c, seed=42)).to(torch.bfloat16).float()
+    xs = nhwc(x)
+    outs = []
+    for _ in range(3):
+        y = torch.empty_like(xs)
+        stats = torch.empty(n, 32, 2, device=dev)
+        ops.groupnorm(ctx, xs, n, h * w, c, gamma, beta, 1e-5, True, y, stats)
+        dx = torch.empty_like(xs)
+        ops.groupnorm_bwd(ctx, xs, n, h * w, c, gamma, beta, True, stats, y, dx)
+        outs.append((y, stats, dx))
+    torch.cuda.synchronize()
+    xg = x.view(n, 32, -1)
+    assert rel(stats[..., 0], xg.mean(-1)) < 1e-4
+    assert rel(stats[..., 1], (xg.var(-1, unbiased=False) + 1e-5).rsqrt()) < 1e-4
+    assert rel(nchw(y, n, h, w), F.silu(F.group_norm(x, 32, gamma, beta, eps=1e-5))) < 1e-2
+    for y2, st2, dx2 in outs[1:]:
+        assert torch.equal(y2, outs[0][0]) and torch.equal(st2, outs[0][1]) and torch.equal(dx2, outs[0][2])
+
+
 @pytest.mark.parametrize("c", [64, 320, 1280])
 def test_layernorm_fwd_bwd(ctx, c):
     from depth_completion_amd import ops

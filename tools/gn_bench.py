@@ -13,8 +13,15 @@ for nb, hw, c in [(1, 6912, 320), (1, 6912, 640), (1, 1728, 640), (1, 432, 1280)
                      ("bwd", lambda: ops.groupnorm_bwd(ctx, x, nb, hw, c, g, b, True, st, dy, dx))]:
         for _ in range(3): fn()
         torch.cuda.synchronize()
+        # 20 calls captured in one graph: device time per call without the host launch path
+        g_ = torch.cuda.CUDAGraph()
+        s_ = torch.cuda.Stream()
+        with torch.cuda.stream(s_):
+            with torch.cuda.graph(g_, stream=s_):
+                for _ in range(20): fn()
+        g_.replay(); torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(20): fn()
+        for _ in range(5): g_.replay()
         e1.record(); torch.cuda.synchronize()
-        print(f"nb={nb} hw={hw} C={c} {name}: {e0.elapsed_time(e1) / 20 * 1e3:.1f} us", flush=True)
+        print(f"nb={nb} hw={hw} C={c} {name}: {e0.elapsed_time(e1) / 100 * 1e3:.1f} us (graph)", flush=True)

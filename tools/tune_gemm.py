@@ -1,5 +1,7 @@
 """Measure the fastest dc_conv_gemm variant for every conv/linear shape of the sampler (GPU).
 
+The committed table is tuned with DC_TUNE_COLD=1 (caches flushed before every timed call).
+
 Runs one eager guided call per workload with Ctx.tune on (each new shape is timed over all tile
 algos x split-K on its real operands) and writes the table that ops.load_tuned() reads.
 
