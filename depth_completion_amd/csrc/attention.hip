@@ -136,6 +136,33 @@ __device__ __forceinline__ bf16x8 trans_frag_at(const char* tile, TrOff o) {
 }
 __device__ __forceinline__ int row_off(int row, int chunk) { return row * 128 + ((chunk ^ tsw(row)) << 4); }
 
+// Transposed fragments by inline-asm ds_read_b64_tr_b16, waited for explicitly (lgkm_wait).  Issued
+// through the builtin, the read carries no alias scope, so the compiler's waitcnt pass assumes it may
+// alias every LDS-DMA in flight and puts a vmcnt(0) in front of it -- draining the ring's prefetch of
+// the next tiles on every tile.  addr: 32-bit LDS address of the lane's row piece; IMM: byte offset.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(unsigned long)((DC_LDS const char*)(p));
+}
+template <int IMM>
+__device__ __forceinline__ bf16x8 trans_frag_nw(unsigned lo, unsigned hi) {
+  bf16x4 a, b;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(a) : "v"(lo), "n"(IMM));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(b) : "v"(hi), "n"(IMM));
+  bf16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+// wait until at most N LDS ops are outstanding; the fragments are operands so no use moves above it
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b, bf16x8& c, bf16x8& d) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "n"(N));
+}
+
 // transposed A-operand fragment from a swizzled tile (same element order as trans_frag)
 __device__ __forceinline__ bf16x8 trans_frag_sw(const char* tile, int key_base, int col_base, int lane) {
   const int g = lane >> 4, i = lane & 15, hh = lane >> 5;
@@ -257,7 +284,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   };
   constexpr int PER_TILE = 2 * TileDma<NT>::MIN_INSTR;  // LDS-DMA instructions per stage, every wave
   int koff[2][4];
-  TrOff voff[4][2];
+  unsigned va[4][2][2];  // LDS addresses of the V^T pieces (the stage offset is an immediate)
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -265,7 +292,11 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int db = 0; db < 2; ++db) voff[s][db] = tr_off(16 * s, 32 * db, lane);
+    for (int db = 0; db < 2; ++db) {
+      const TrOff o = tr_off(16 * s, 32 * db, lane);
+      va[s][db][0] = lds_addr(ring) + o.lo;
+      va[s][db][1] = lds_addr(ring) + o.hi;
+    }
   for (int i = 0; i < S - 1 && i < mine; ++i) issue(i);
   // the ring stage is a compile-time constant in each copy of the body (ds_read immediate offsets)
   auto step = [&](int i, auto STC) __attribute__((always_inline)) {
@@ -327,12 +358,28 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
       }
       l += ps;
       m = mnew;
+      // V^T fragments: two k-slices in flight ahead of the MFMAs that consume them
+      constexpr int VIMM = ST * FwdLds<QW, KS>::STAGE + TILE_B;
+      bf16x8 vf[4][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int db = 0; db < 2; ++db) vf[s][db] = trans_frag_nw<VIMM>(va[s][db][0], va[s][db][1]);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
+        if (s + 2 < 4) {
+#pragma unroll
+          for (int db = 0; db < 2; ++db) vf[s + 2][db] = trans_frag_nw<VIMM>(va[s + 2][db][0], va[s + 2][db][1]);
+          lgkm_wait<8>(vf[s][0], vf[s][1]);
+        } else if (s == 2) {
+          lgkm_wait<4>(vf[s][0], vf[s][1]);
+        } else {
+          lgkm_wait<0>(vf[s][0], vf[s][1]);
+        }
         const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
 #pragma unroll
         for (int db = 0; db < 2; ++db)
-          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(vt_s, voff[s][db]), pf, oacc[db], 0, 0, 0);
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], pf, oacc[db], 0, 0, 0);
       }
     }
   };
@@ -481,7 +528,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   };
   // per-lane LDS offsets (loop-invariant)
   int qoff[2][4];
-  TrOff toff[2][2][2];
+  unsigned ta[2][2][2][2];  // LDS addresses of the transposed pieces (tile + stage offsets are immediates)
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
@@ -489,7 +536,11 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int db = 0; db < 2; ++db) toff[qb][s2][db] = tr_off(32 * qb + 16 * s2, 32 * db, lane);
+      for (int db = 0; db < 2; ++db) {
+        const TrOff o = tr_off(32 * qb + 16 * s2, 32 * db, lane);
+        ta[qb][s2][db][0] = lds_addr(ring) + o.lo;
+        ta[qb][s2][db][1] = lds_addr(ring) + o.hi;
+      }
   }
   constexpr int PER_TILE = 2 * TileDma<NT>::MIN_INSTR;
   constexpr float L8 = LOG2E * 0.125f;
@@ -517,6 +568,14 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(dt_s + qoff[qb][s]), vf[s],
                                                        dp, 0, 0, 0);
         }
+        // dO^T / Q^T fragments of the first k-slice, in flight under the softmax
+        constexpr int QIMM = ST * STG, DIMM = ST * STG + TILE_B;
+        bf16x8 fv[2][2], fk[2][2];
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          fv[0][db] = trans_frag_nw<DIMM>(ta[qb][0][db][0], ta[qb][0][db][1]);
+          fk[0][db] = trans_frag_nw<QIMM>(ta[qb][0][db][0], ta[qb][0][db][1]);
+        }
         // P = exp2(S_raw log2e / 8 - lse log2e); dS = P * (dP - delta)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -530,13 +589,20 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
           }
         }
 #pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          fv[1][db] = trans_frag_nw<DIMM>(ta[qb][1][db][0], ta[qb][1][db][1]);
+          fk[1][db] = trans_frag_nw<QIMM>(ta[qb][1][db][0], ta[qb][1][db][1]);
+        }
+#pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
+          if (s2 == 0) lgkm_wait<8>(fv[0][0], fv[0][1], fk[0][0], fk[0][1]);
+          else lgkm_wait<0>(fv[1][0], fv[1][1], fk[1][0], fk[1][1]);
           const bf16x8 pf = acc_to_frag(sp, s2);
           const bf16x8 sf = acc_to_frag(dp, s2);
 #pragma unroll
           for (int db = 0; db < 2; ++db) {
-            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(dt_s, toff[qb][s2][db]), pf, dv[db], 0, 0, 0);
-            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(qt_s, toff[qb][s2][db]), sf, dk[db], 0, 0, 0);
+            dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fv[s2][db], pf, dv[db], 0, 0, 0);
+            dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk[s2][db], sf, dk[db], 0, 0, 0);
           }
         }
       }
@@ -649,7 +715,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
     dma.issue(rv, st + TILE_B, (tb + i) * 64, T, ld, lt);
   };
   int koff[2][4];
-  TrOff toff[2][2][2];
+  unsigned ta[2][2][2][2];  // LDS addresses of the K^T pieces (the stage offset is an immediate)
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
 #pragma unroll
@@ -657,7 +723,11 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int db = 0; db < 2; ++db) toff[b][s2][db] = tr_off(32 * b + 16 * s2, 32 * db, lane);
+      for (int db = 0; db < 2; ++db) {
+        const TrOff o = tr_off(32 * b + 16 * s2, 32 * db, lane);
+        ta[b][s2][db][0] = lds_addr(ring) + o.lo;
+        ta[b][s2][db][1] = lds_addr(ring) + o.hi;
+      }
   }
   constexpr int PER_TILE = 2 * TileDma<NT>::MIN_INSTR;
   for (int i = 0; i < S - 1 && i < mine; ++i) issue(i);
@@ -681,6 +751,13 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(vt_s + koff[b][s]), df[s], dp,
                                                        0, 0, 0);
         }
+        // K^T fragments in flight under the softmax
+        constexpr int KIMM = ST * STG;
+        bf16x8 fq[2][2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int db = 0; db < 2; ++db) fq[s2][db] = trans_frag_nw<KIMM>(ta[b][s2][db][0], ta[b][s2][db][1]);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float pv = fast_exp2(fmaf(sp[r], LOG2E, -my_lse));
@@ -694,10 +771,12 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
+          if (s2 == 0) lgkm_wait<4>(fq[0][0], fq[0][1]);
+          else lgkm_wait<0>(fq[1][0], fq[1][1]);
           const bf16x8 sf = acc_to_frag(sp, s2);
 #pragma unroll
           for (int db = 0; db < 2; ++db)
-            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trans_frag_at(kt_s, toff[b][s2][db]), sf, dq[db], 0, 0, 0);
+            dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq[s2][db], sf, dq[db], 0, 0, 0);
         }
       }
     }
