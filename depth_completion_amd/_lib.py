@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -70,6 +70,8 @@ _SIGS = {
     "dc_final_dense": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp],
     "dc_ddim_step": [vp, vp, i32, i32, vp, vp, vp],
     "dc_closed_form_affine": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp],
+    "dc_sparse_loss_cf": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp],
+    "dc_affine_fit": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, f32, vp, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],
 }
 _RESTYPE = {"dc_groupnorm_ws_bytes": i64}

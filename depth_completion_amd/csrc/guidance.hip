@@ -41,7 +41,8 @@ __device__ float block_min(float v, float* scratch) {
 }
 __device__ float block_max(float v, float* scratch) { return -block_min(-v, scratch); }
 
-// params per frame: [0]=lo [1]=hi (metres) [2]=lo_p [3]=hi_p [4]=min_g [5]=max_g
+// params per frame: [0]=lo [1]=hi (metres) [2]=lo_p [3]=hi_p [4]=min_g [5]=max_g [6]=count
+// [7]=projection + 4 inv (the depth space the loss compares in)
 __global__ void sparse_setup_kernel(const float* sparse, int H, int W, int norm, float min_depth, float max_depth,
                                     const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt,
                                     float* params) {
@@ -122,7 +123,7 @@ __global__ void sparse_setup_kernel(const float* sparse, int H, int W, int norm,
     cnt[n] = count;
     float* pr = params + n * 8;
     pr[0] = lo; pr[1] = hi; pr[2] = lo_p; pr[3] = hi_p; pr[4] = gmin; pr[5] = gmax;
-    pr[6] = (float)count; pr[7] = 0.0f;
+    pr[6] = (float)count; pr[7] = (float)(projection + 4 * inv);  // the loss's depth space (DSpace)
   }
 }
 
@@ -209,6 +210,36 @@ __device__ __forceinline__ float sample_affine(const bf16* out, int ldo, int n, 
   return (float)(bf16)v;
 }
 
+// Depth space of the loss (marigold_dc.py:843-860, 930-948): the clamped normalised depth G goes back to
+// metres, through the projection (log / log10) and / or the inverse, and is renormalised with the
+// projected bounds; returns that value and dN/dG.  The identity for linear without inverse.
+struct DSpace {
+  int proj, inv;
+  float lo, hi, lo_p, hi_p;
+  __device__ explicit DSpace(const float* pr) {
+    const int code = (int)pr[7];
+    proj = code & 3;
+    inv = code >> 2;
+    lo = pr[0]; hi = pr[1]; lo_p = pr[2]; hi_p = pr[3];
+  }
+  __device__ float operator()(float G, float& dNdG) const {
+    if (proj == 0 && !inv) {
+      dNdG = 1.0f;
+      return G;
+    }
+    const float span = hi - lo;
+    const float D = G * span + lo;
+    float P = D, dP = 1.0f;
+    if (proj == 1) { P = logf(D); dP = 1.0f / D; }
+    else if (proj == 2) { P = log10f(D); dP = 1.0f / (D * 2.302585093f); }
+    float Q = P, dQ = 1.0f;
+    if (inv) { Q = 1.0f / P; dQ = -1.0f / (P * P); }
+    const float den = hi_p - lo_p;
+    dNdG = (dQ * dP * span) / den;
+    return (Q - lo_p) / den;
+  }
+};
+
 // one block per frame.  affine[n*2] = scale, affine[n*2+1] = shift (fp32 trainables)
 __global__ void sparse_loss_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
                                    const int* idx, const float* gval, const int* cnt, const float* params,
@@ -226,17 +257,19 @@ __global__ void sparse_loss_kernel(const bf16* out, int ldo, int PH, int PW, int
   const float inv_cnt = 1.0f / (float)count;
   float sum_db = 0.0f, sum_de = 0.0f, lsum = 0.0f;
   float* dAn = dA + (long)n * PH * PW;
+  const DSpace ds(pr);
   for (int k = threadIdx.x; k < count; k += blockDim.x) {
     const int p = idx[n * HW + k];
     const int y = p / W, x = p - (p / W) * W;
     Taps t;
     const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t);
     const float F = B * aff + E;
-    const float G = fminf(fmaxf(F, 0.0f), 1.0f);
-    const float r = G - gval[n * HW + k];
+    float dNdG;
+    const float Nv = ds(fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
+    const float r = Nv - gval[n * HW + k];
     lsum += fabsf(r) * inv_cnt + (r * r) * inv_cnt;
     const float sg = (r > 0.0f) ? 1.0f : ((r < 0.0f) ? -1.0f : 0.0f);
-    const float dG = sg * inv_cnt + 2.0f * r * inv_cnt;
+    const float dG = (sg * inv_cnt + 2.0f * r * inv_cnt) * dNdG;
     const float dF = (F >= 0.0f && F <= 1.0f) ? dG : 0.0f;
     sum_db += dF * aff;
     sum_de += dF;
@@ -468,6 +501,172 @@ __global__ void closed_form_kernel(const bf16* out, int ldo, int PH, int PW, int
   }
 }
 
+// Guided steps with closed_form=True (marigold_dc.py:332-336 inside the per-step loop :828-877): the
+// affine fit s, t = compute_affine_params(A) of the current preview is differentiated too.  Forward as
+// closed_form_kernel; with e_k = dL/dd_k (l1 + l2, clamp(0, 1) mask), Gs = sum e_k (a_k - mean a),
+// E = sum e_k, V the masked variance, centred a / g written ac_k / gc_k:
+//   dL/da_k = s e_k + Gs (gc_k - 2 s ac_k) / (V + eps) - s E / K
+// scattered through the bilinear taps into dA like sparse_loss_kernel.  One block per frame.
+__global__ void sparse_loss_cf_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
+                                      const int* idx, const float* gval, const int* cnt, const float* params,
+                                      float* dA, float* loss) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.x;
+  const long HW = (long)H * W;
+  const int count = cnt[n];
+  const int* ix = idx + n * HW;
+  const float* gv = gval + n * HW;
+  auto aff_at = [&](int k, Taps& t) {
+    const int p = ix[k];
+    return sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t);
+  };
+  float sa = 0.0f, sg = 0.0f;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    Taps t;
+    sa += aff_at(k, t);
+    sg += gv[k];
+  }
+  const float sum_a = (float)(bf16)block_sum(sa, scratch);
+  __syncthreads();
+  const float sum_g = block_sum(sg, scratch);
+  __syncthreads();
+  const float K = (float)count;
+  const float ma = (float)(bf16)(sum_a / K);
+  const float mg = sum_g / K;
+  float sv = 0.0f, sc = 0.0f;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    Taps t;
+    const float ac = (float)(bf16)(aff_at(k, t) - ma);
+    sv += (float)(bf16)(ac * ac);
+    sc += ac * (gv[k] - mg);
+  }
+  const float var = (float)(bf16)block_sum(sv, scratch);
+  __syncthreads();
+  const float cov = block_sum(sc, scratch);
+  __syncthreads();
+  const float vpe = (float)(bf16)(var + 1e-7f);
+  const float scale = cov / vpe;
+  const float shift = mg - scale * ma;
+  const float inv_cnt = 1.0f / K;
+  const DSpace ds(params + n * 8);
+  float se = 0.0f, sge = 0.0f, lsum = 0.0f;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    Taps t;
+    const float a = aff_at(k, t);
+    const float F = scale * a + shift;
+    float dNdG;
+    const float Nv = ds(fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
+    const float r = Nv - gv[k];
+    lsum += fabsf(r) * inv_cnt + (r * r) * inv_cnt;
+    const float sgn = (r > 0.0f) ? 1.0f : ((r < 0.0f) ? -1.0f : 0.0f);
+    const float dF = (F >= 0.0f && F <= 1.0f) ? (sgn * inv_cnt + 2.0f * r * inv_cnt) * dNdG : 0.0f;
+    se += dF;
+    sge += dF * (a - ma);
+  }
+  const float E = block_sum(se, scratch);
+  __syncthreads();
+  const float Gs = block_sum(sge, scratch);
+  __syncthreads();
+  const float ls = block_sum(lsum, scratch);
+  float* dAn = dA + (long)n * PH * PW;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    Taps t;
+    const float a = aff_at(k, t);
+    const float F = scale * a + shift;
+    float dNdG;
+    const float Nv = ds(fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
+    const float r = Nv - gv[k];
+    const float sgn = (r > 0.0f) ? 1.0f : ((r < 0.0f) ? -1.0f : 0.0f);
+    const float e = (F >= 0.0f && F <= 1.0f) ? (sgn * inv_cnt + 2.0f * r * inv_cnt) * dNdG : 0.0f;
+    const float ac = (float)(bf16)(a - ma);
+    const float gc = gv[k] - mg;
+    const float dff = (float)(bf16)(scale * e + Gs * (gc - 2.0f * scale * ac) / vpe - scale * E * inv_cnt);
+    if (t.ly1 == 0.0f && t.lx1 == 0.0f && t.y0 == t.y1 && t.x0 == t.x1) {
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x0], dff);
+    } else {
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x0], t.ly0 * t.lx0 * dff);
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x1], t.ly0 * t.lx1 * dff);
+      atomicAdd(&dAn[(long)t.y1 * PW + t.x0], t.ly1 * t.lx0 * dff);
+      atomicAdd(&dAn[(long)t.y1 * PW + t.x1], t.ly1 * t.lx1 * dff);
+    }
+  }
+  if (threadIdx.x == 0) loss[n] = ls;
+}
+
+// Per-input training (train_method="per-input", marigold_dc.py:911-967) with learned affine params: the
+// reference's optimiser still holds the pre-loop latent tensor (:777-783 vs :913), so only scale / shift
+// move; the decode A of the final latents is fixed, and each of the train_steps iterations is the l1 + l2
+// loss on the UNclamped s^2 (max - min) A + sh^2 min at the sparse pixels followed by one fp32 Adam step
+// (torch.optim.Adam arithmetic, step count 1..train_steps).  One block per frame, all steps in one launch.
+__global__ void affine_fit_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
+                                  const int* idx, const float* gval, const int* cnt, const float* params,
+                                  int train_steps, float lr, float* affine, float* loss) {
+  __shared__ float scratch[16];
+  __shared__ float s_aff[2];
+  const int n = blockIdx.x;
+  const long HW = (long)H * W;
+  const int count = cnt[n];
+  const int* ix = idx + n * HW;
+  const float* gv = gval + n * HW;
+  const float* pr = params + n * 8;
+  const float gmin = pr[4], gmax = pr[5];
+  const float inv_cnt = 1.0f / (float)count;
+  const DSpace ds(pr);
+  const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
+  float m0 = 0.0f, v0 = 0.0f, m1 = 0.0f, v1 = 0.0f;
+  if (threadIdx.x == 0) {
+    s_aff[0] = affine[n * 2];
+    s_aff[1] = affine[n * 2 + 1];
+  }
+  __syncthreads();
+  double b1p = 1.0, b2p = 1.0;
+  for (int it = 1; it <= train_steps; ++it) {
+    const float s = s_aff[0], sh = s_aff[1];
+    const float B = (s * s) * (gmax - gmin);
+    const float E = (sh * sh) * gmin;
+    float sum_db = 0.0f, sum_de = 0.0f, lsum = 0.0f;
+    for (int k = threadIdx.x; k < count; k += blockDim.x) {
+      const int p = ix[k];
+      Taps t;
+      const float a = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t);
+      const float F = B * a + E;
+      float dNdF;
+      const float Nv = ds(F, dNdF);
+      const float r = Nv - gv[k];
+      lsum += fabsf(r) * inv_cnt + (r * r) * inv_cnt;
+      const float sgn = (r > 0.0f) ? 1.0f : ((r < 0.0f) ? -1.0f : 0.0f);
+      const float dF = (sgn * inv_cnt + 2.0f * r * inv_cnt) * dNdF;
+      sum_db += dF * a;
+      sum_de += dF;
+    }
+    const float db = block_sum(sum_db, scratch);
+    __syncthreads();
+    const float de = block_sum(sum_de, scratch);
+    __syncthreads();
+    const float ls = block_sum(lsum, scratch);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      b1p *= 0.9;
+      b2p *= 0.999;
+      const float step_size = (float)(lr / (1.0 - b1p));
+      const float bc2s = (float)sqrt(1.0 - b2p);
+      const float g0 = db * (gmax - gmin) * (2.0f * s), g1 = (de * gmin) * (2.0f * sh);
+      m0 = m0 + beta1w * (g0 - m0);
+      v0 = v0 * beta2 + one_m_b2 * g0 * g0;
+      m1 = m1 + beta1w * (g1 - m1);
+      v1 = v1 * beta2 + one_m_b2 * g1 * g1;
+      s_aff[0] = s + (-step_size) * (m0 / (sqrtf(v0) / bc2s + eps));
+      s_aff[1] = sh + (-step_size) * (m1 / (sqrtf(v1) / bc2s + eps));
+      loss[n] = ls;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    affine[n * 2] = s_aff[0];
+    affine[n * 2 + 1] = s_aff[1];
+  }
+}
+
 inline dim3 grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 65536) b = 65536;
@@ -579,5 +778,28 @@ extern "C" int dc_closed_form_affine(const void* dec_out, int ldo, int nb, int p
 extern "C" int dc_memset_async(void* ptr, int value, long long bytes, void* stream) {
   if (!ptr || bytes < 0) return DC_ERR_ARG;
   if (hipMemsetAsync(ptr, value, (size_t)bytes, (hipStream_t)stream) != hipSuccess) return DC_ERR_LAUNCH;
+  return DC_OK;
+}
+
+extern "C" int dc_sparse_loss_cf(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                                 const int* idx, const float* gval, const int* cnt, const float* params, float* dA,
+                                 float* loss, void* stream) {
+  if (!dec_out || !idx || !gval || !cnt || !params || !dA || !loss || nb <= 0 || rh > ph || rw > pw)
+    return DC_ERR_ARG;
+  hipLaunchKernelGGL(sparse_loss_cf_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo,
+                     ph, pw, rh, rw, h, w, idx, gval, cnt, params, dA, loss);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_affine_fit(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                             const int* idx, const float* gval, const int* cnt, const float* params, int train_steps,
+                             float lr, float* affine, float* loss, void* stream) {
+  if (!dec_out || !idx || !gval || !cnt || !params || !affine || !loss || nb <= 0 || train_steps <= 0 ||
+      rh > ph || rw > pw)
+    return DC_ERR_ARG;
+  hipLaunchKernelGGL(affine_fit_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
+                     pw, rh, rw, h, w, idx, gval, cnt, params, train_steps, lr, affine, loss);
+  DC_CHECK_LAUNCH();
   return DC_OK;
 }

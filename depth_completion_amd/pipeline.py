@@ -171,25 +171,27 @@ class MarigoldDepthCompletionPipeline:
             raise ValueError(f"Unknown optimizer: {opt}")
         lr_latent, lr_scaling = (0.05, 0.005) if lr is None else lr
         loss_funcs = ["l1", "l2"] if loss_funcs is None else list(loss_funcs)
-        # the hot path of this build (SURVEY.md §8 defaults); other modes are §8(f) "next" rows
-        # train_latents=False (+ closed form) is the plain DDIM sampler with the closed-form fit at the end
-        # (marigold_dc.py:905-909, 969-985): no optimiser, loss or guidance settings take part in it
-        guided = train_latents
+        # Modes (marigold_dc.py:758-967), all on the same kernels:
+        #  guided    train_latents, per-step: the guided DDIM loop (learned affine, or closed_form=True with
+        #            the fit differentiated: dc_sparse_loss_cf)
+        #  per-input train_latents, per-input: plain DDIM loop, then train_steps optimiser steps which --
+        #            as the reference's optimiser holds the pre-loop latent tensor (:777-783 vs :913) -- move
+        #            only the learned scale / shift (dc_affine_fit); with closed_form nothing moves at all
+        #  plain     train_latents=False: plain DDIM loop + closed-form fit at the end (:905-909, 969-985)
+        guided = train_latents and train_method == "per-step"
+        fit_affine = train_latents and train_method == "per-input" and not closed_form
+        optimised = guided or fit_affine
         unsupported = []
-        if guided and closed_form:
-            unsupported.append("closed_form with train_latents=True")
-        if guided and train_method != "per-step":
-            unsupported.append("train_method=per-input")
-        if guided and opt != "adam":
+        if optimised and opt != "adam":
             unsupported.append(f"opt={opt}")
-        if guided and kld:
+        if guided and kld:   # (per-input: the KL term reaches only the latents, which do not move)
             unsupported.append("kld")
-        if guided and sorted(loss_funcs) != ["l1", "l2"]:
+        if optimised and sorted(loss_funcs) != ["l1", "l2"]:
             unsupported.append(f"loss_funcs={loss_funcs}")
         if interp_mode != "bilinear":
             unsupported.append(f"interp_mode={interp_mode}")
         if unsupported:
-            raise NotImplementedError("HIP path supports the predict.py default guided mode only; got "
+            raise NotImplementedError("HIP path supports Adam with the l1 + l2 loss for the optimised modes; got "
                                       + ", ".join(unsupported))
         dev = self.device
         ctx = self.ctx
@@ -242,26 +244,25 @@ class MarigoldDepthCompletionPipeline:
         if (cnt_host == 0).any():
             raise ValueError("No valid values found in mask for some positions. "
                              "Ensure that mask has at least one True value along the specified dimensions.")
-        if guided and (projection != "linear" or inv):
-            raise NotImplementedError("non-linear depth space in the loss is a next-round row (SURVEY §8f)")
 
         # ---- per-call tables
         ts = self.scheduler.timesteps(steps)
         coef = self.scheduler.coef(steps).to(dev)
         adam = adam_table(steps, lr_latent, lr_scaling).to(dev)
         self.unet.build_temb_tables(ctx, ts)
-        for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"]):
+        for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"], st["daff"]):
             ops.memset(ctx, t)
         st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))
         ops.memset(ctx, ctx.step)
+        cf = bool(closed_form)
         self._call_state = dict(idx=idx, gval=gval, cnt=cnt, params=params, coef=coef, adam=adam, H=H, W=W, RH=RH,
-                                RW=RW, PH=PH, PW=PW, n=n, h=h, w=w)
+                                RW=RW, PH=PH, PW=PW, n=n, h=h, w=w, cf=cf)
 
         # ---- denoising loop (marigold_dc.py:800-909): guided steps, or plain DDIM steps
         step_fn = self._step if guided else self._ddim_step
         if self.use_graph:
             g = st["graph"]
-            gkey = (guided, steps, H, W, RH, RW, lr_latent, lr_scaling)
+            gkey = (guided, guided and cf, steps, H, W, RH, RW, lr_latent, lr_scaling)
             if g is None or st["graph_key"] != gkey:
                 # tables are rebuilt per call at new addresses: capture against this call's buffers
                 g = torch.cuda.CUDAGraph()
@@ -294,6 +295,10 @@ class MarigoldDepthCompletionPipeline:
         dp.forward()
         dense = torch.empty(n, 1, H, W, dtype=torch.float32, device=dev)
         cs = self._tables(st)
+        if fit_affine:   # per-input training of scale / shift on the (fixed) final decode (:911-967)
+            _lib.call("dc_affine_fit", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["idx"].data_ptr(),
+                      cs["gval"].data_ptr(), cs["cnt"].data_ptr(), cs["params"].data_ptr(), int(train_steps),
+                      float(lr_scaling), st["affine"].data_ptr(), st["loss"].data_ptr(), ctx.stream)
         if closed_form:   # compute_affine_params on the final decode (marigold_dc.py:332-336)
             _lib.call("dc_closed_form_affine", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["idx"].data_ptr(),
                       cs["gval"].data_ptr(), cs["cnt"].data_ptr(), st["affine"].data_ptr(), ctx.stream)
@@ -347,9 +352,15 @@ class MarigoldDepthCompletionPipeline:
                   st["x0"].data_ptr(), dp.tin.data_ptr(), st["eps_norm"].data_ptr(), s)
         dp.forward()                                                         # TAESD decode of x0
         ops.memset(ctx, st["dA"])
-        _lib.call("dc_sparse_loss", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"], cs["W"],
-                  cs["idx"].data_ptr(), cs["gval"].data_ptr(), cs["cnt"].data_ptr(), cs["params"].data_ptr(),
-                  st["affine"].data_ptr(), st["dA"].data_ptr(), st["daff"].data_ptr(), st["loss"].data_ptr(), s)
+        if cs["cf"]:   # closed-form fit of the preview, differentiated (daff stays zero: no learned affine)
+            _lib.call("dc_sparse_loss_cf", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"],
+                      cs["W"], cs["idx"].data_ptr(), cs["gval"].data_ptr(), cs["cnt"].data_ptr(),
+                      cs["params"].data_ptr(), st["dA"].data_ptr(), st["loss"].data_ptr(), s)
+        else:
+            _lib.call("dc_sparse_loss", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"],
+                      cs["W"], cs["idx"].data_ptr(), cs["gval"].data_ptr(), cs["cnt"].data_ptr(),
+                      cs["params"].data_ptr(), st["affine"].data_ptr(), st["dA"].data_ptr(), st["daff"].data_ptr(),
+                      st["loss"].data_ptr(), s)
         _lib.call("dc_decode_tail_bwd", dp.out.data_ptr(), 8, st["dA"].data_ptr(), n, cs["PH"], cs["PW"], cs["RH"],
                   cs["RW"], dp.dout.data_ptr(), s)
         dp.backward()                                                        # d tin

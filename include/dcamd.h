@@ -119,6 +119,8 @@ int dc_nchw_to_nhwc(const void* x, int nb, long long hw, int c, void* y, int ldy
  * 1 log, 2 log10.  params[nb][8] = lo, hi, lo_p, hi_p, min_g, max_g, count, 0.
  * coef[step][4] = sqrt(a_t), sqrt(1-a_t), sqrt(a_prev), sqrt(1-a_prev);
  * adam_tab[step][4] = lr_latent/bc1, sqrt(bc2), lr_affine/bc1, 0.
+ * params[nb][8] (dc_sparse_setup) = lo, hi, lo_p, hi_p, min_g, max_g, count, projection + 4 inv: the losses
+ * compare in the projected / inverted depth space it names (marigold_dc.py:843-860).
  */
 int dc_sparse_setup(const float* sparse, int nb, int h, int w, int norm, float min_depth, float max_depth,
                     const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt, float* params,
@@ -143,6 +145,16 @@ int dc_ddim_step(void* x8, const void* v, int nb, int hw, const float* coef, con
 /* compute_affine_params (marigold_dc.py:53-128) over the sparse pixels: affine[nb][2] = scale, shift */
 int dc_closed_form_affine(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
                           const int* idx, const float* gval, const int* cnt, float* affine, void* stream);
+/* guided steps with closed_form=True (marigold_dc.py:332-336 inside :828-877): loss of the closed-form fit
+ * of the preview and its gradient dA, the fit (s, t) included in the differentiation */
+int dc_sparse_loss_cf(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                      const int* idx, const float* gval, const int* cnt, const float* params, float* dA, float* loss,
+                      void* stream);
+/* train_method="per-input" with learned affine (marigold_dc.py:911-967): train_steps Adam steps on
+ * affine[nb][2] (scale, shift) against the fixed decode of the final latents */
+int dc_affine_fit(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w, const int* idx,
+                  const float* gval, const int* cnt, const float* params, int train_steps, float lr, float* affine,
+                  float* loss, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
 
 #ifdef __cplusplus

@@ -161,3 +161,63 @@ def test_plain_ddim_closed_form(kw):
     lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
     print(f"\nplain DDIM {kw}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
     assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
+
+
+def _mode_parity(args, seed, label, fitted=False):
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    n, h, w, res = 2, 48, 64, 64
+    cfg_o = tiny_unet_config()
+    imgs, sparses = synth_inputs(n, h, w, 60, seed=seed)
+    noise = torch.randn((1, 4, 6, 8), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
+    args = dict(args, resolution=res, init_noise=noise)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
+    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
+    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dh).all() and dh.shape == d32.shape and lh.shape == l32.shape
+    lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
+    lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
+    if fitted:
+        err_h, p99_h = fitted_error(dh, d32, sparses)
+        err_b, p99_b = fitted_error(d16, d32, sparses)
+    else:
+        rng = (d32.amax(dim=(1, 2, 3)) - d32.amin(dim=(1, 2, 3))).view(-1, 1, 1, 1)
+        err_h = float(((dh - d32).abs() / rng).mean())
+        err_b = float(((d16 - d32).abs() / rng).mean())
+    print(f"\n{label}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
+    assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
+    return pipe
+
+
+def test_guided_closed_form():
+    """closed_form=True with trainable latents (per-step): the closed-form fit of every preview is part of
+    the differentiated loss (marigold_dc.py:332-336 inside :828-877)."""
+    _mode_parity(dict(norm="const", steps=8, closed_form=True), 21, "guided closed-form", fitted=True)
+
+
+@pytest.mark.parametrize("closed_form", [None, True])
+def test_per_input(closed_form):
+    """train_method="per-input" (marigold_dc.py:911-967): plain DDIM loop, then train_steps optimiser steps
+    that move only the learned scale / shift (the optimiser holds the pre-loop latent tensor)."""
+    pipe = _mode_parity(dict(norm="minmax", steps=6, train_method="per-input", train_steps=12,
+                             closed_form=closed_form), 22, f"per-input closed_form={closed_form}")
+    if closed_form is None:
+        assert torch.isfinite(pipe.last_loss).all()
+
+
+@pytest.mark.parametrize("kw", [dict(norm="minmax", projection="log10", min_depth=1.0),
+                                dict(norm="const", projection="log", min_depth=2.0),
+                                dict(norm="minmax", inv=True, min_depth=1.0),
+                                dict(norm="minmax", inv=True, min_depth=1.0, closed_form=True)])
+def test_guided_depth_space(kw):
+    """Guided steps with the loss in a projected / inverted depth space (marigold_dc.py:843-860)."""
+    _mode_parity(dict(kw, steps=6), 23, f"guided {kw}", fitted=True)
+
+
+def test_per_input_projected():
+    _mode_parity(dict(norm="minmax", projection="log", min_depth=1.0, steps=5, train_method="per-input",
+                      train_steps=8), 24, "per-input log")
