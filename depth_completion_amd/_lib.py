@@ -64,14 +64,14 @@ _SIGS = {
     "dc_preview": [vp, vp, i32, i32, vp, vp, vp, vp, vp, vp],
     "dc_sparse_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dc_decode_tail_bwd": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp],
-    "dc_latent_update": [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp],
+    "dc_latent_update": [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp],
     "dc_step_advance": [vp, i32, vp],
     "dc_latent_init": [vp, vp, f32, i32, i32, vp, vp],
     "dc_final_dense": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp],
     "dc_ddim_step": [vp, vp, i32, i32, vp, vp, vp],
     "dc_closed_form_affine": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp],
     "dc_sparse_loss_cf": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp],
-    "dc_affine_fit": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, f32, vp, vp, vp],
+    "dc_affine_fit": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, f32, i32, vp, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],
 }
 _RESTYPE = {"dc_groupnorm_ws_bytes": i64}

@@ -9,8 +9,9 @@
 //                       sparse pixels only, learned affine + clamp, l1+l2 loss, its gradient
 //                       scattered into the decoded-depth image, d(scale), d(shift)  (:829-877)
 //   dc_decode_tail_bwd  gradient of the decode tail back to the TAESD decoder output
-//   dc_latent_update    grad accumulation, ||eps||/||g|| rescale, Adam (bf16 state for the latent,
-//                       fp32 for scale/shift), DDIM prev-sample on the post-Adam latent (:879-904)
+//   dc_latent_update    grad accumulation (+ KL term), ||eps||/||g|| rescale, Adam / SGD / Adagrad (bf16
+//                       state for the latent, fp32 for scale/shift), DDIM prev-sample on the updated latent
+//                       (:879-904)
 //   dc_final_dense      final decode -> affine -> clamp -> metres (:969-985)
 // Elementwise arithmetic mirrors PyTorch's op-by-op rounding (bf16 results of bf16 ops, fp32 for
 // the affine/loss), so the only deviation from the reference is reduction order.
@@ -323,22 +324,60 @@ __global__ void decode_tail_bwd_kernel(const bf16* out, int ldo, const float* dA
 }
 
 // adam_tab per step: [step_size = lr_lat/bc1, bc2_sqrt, step_size_aff = lr_aff/bc1, unused]
+// KL term of compute_loss (kld=True, marigold_dc.py:239-243 -> utils.kld_stdnorm, utils.py:28-86) on the
+// bf16 latent x, per frame over M = 4 hw elements: mode 1 "simple" mean(x^2) -> 2x/M; mode 2 "strict"
+// 0.5 (mu^2 + var - log(var + eps) - 1) -> mu/M + (x - mu)/M (1 - 1/(var + eps)), eps = bf16 eps; times
+// kld_weight, as autograd forms it in bf16.
+struct Kld {
+  int mode;
+  float w, mu, var_eps, inv_m;
+  __device__ float grad(float x) const {
+    if (mode == 1) return (float)(bf16)((float)(bf16)((float)(bf16)w * inv_m) * (2.0f * x));
+    const float d = (float)(bf16)((x - mu) * inv_m);
+    return (float)(bf16)(w * (float)(bf16)(mu * inv_m + d * (1.0f - 1.0f / var_eps)));
+  }
+};
+
+// opt: 0 Adam (bf16 state m_lat / v_lat), 1 SGD (no state), 2 Adagrad (bf16 state sum in m_lat); the
+// affine scalars take the same rule in fp32.  tab per step: Adam [lr_lat/bc1, sqrt(bc2), lr_aff/bc1, 0],
+// SGD / Adagrad [lr_lat, 0, lr_aff, 0].
 __global__ void latent_update_kernel(bf16* x8, const bf16* v, const bf16* gdir, const bf16* gunet, int hw,
                                      const float* coef, const float* adam_tab, const int* step,
                                      const float* eps_norm, bf16* m_lat, bf16* v_lat, float* affine,
-                                     float* m_aff, float* v_aff, const float* daff_grad, float* dbg) {
+                                     float* m_aff, float* v_aff, const float* daff_grad, float* dbg, int opt,
+                                     int kld_mode, float kld_weight) {
   __shared__ float scratch[16];
   const int n = blockIdx.x;
   const int st = *step;
   const float sa = coef[st * 4 + 0], sb = coef[st * 4 + 1], sap = coef[st * 4 + 2], sbp = coef[st * 4 + 3];
   const float step_size = adam_tab[st * 4 + 0], bc2s = adam_tab[st * 4 + 1], step_aff = adam_tab[st * 4 + 2];
   const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
+  Kld kl{kld_mode, kld_weight, 0.0f, 1.0f, 1.0f / (4.0f * hw)};
+  if (kld_mode == 2) {  // mean / biased variance of the latent (bf16 reductions)
+    float s1 = 0.0f;
+    for (int i = threadIdx.x; i < hw * 4; i += blockDim.x) s1 += (float)x8[((long)n * hw + (i >> 2)) * 8 + 4 + (i & 3)];
+    kl.mu = (float)(bf16)(block_sum(s1, scratch) * kl.inv_m);
+    __syncthreads();
+    float s2 = 0.0f;
+    for (int i = threadIdx.x; i < hw * 4; i += blockDim.x) {
+      const float d = (float)x8[((long)n * hw + (i >> 2)) * 8 + 4 + (i & 3)] - kl.mu;
+      s2 += d * d;
+    }
+    const float var = (float)(bf16)(block_sum(s2, scratch) * kl.inv_m);
+    kl.var_eps = (float)(bf16)(var + 0.0078125f);
+    __syncthreads();
+  }
+  auto grad_at = [&](long pix, int k) {
+    float g = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
+    if (kld_mode) g = (float)(bf16)(g + kl.grad((float)x8[pix * 8 + 4 + k]));
+    return g;
+  };
   // pass 1: ||g||
   float ss = 0.0f;
   for (int i = threadIdx.x; i < hw * 4; i += blockDim.x) {
     const long pix = (long)n * hw + (i >> 2);
     const int k = i & 3;
-    const float g = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
+    const float g = grad_at(pix, k);
     ss += g * g;
   }
   const float gn = (float)(bf16)sqrtf(block_sum(ss, scratch));
@@ -350,19 +389,29 @@ __global__ void latent_update_kernel(bf16* x8, const bf16* v, const bf16* gdir, 
     const long pix = (long)n * hw + (i >> 2);
     const int k = i & 3;
     const long e = pix * 4 + k;
-    float g = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
+    float g = grad_at(pix, k);
     g = (float)(bf16)(g * factor);
-    float m = (float)m_lat[e], vv = (float)v_lat[e];
-    m = (float)(bf16)(m + beta1w * (g - m));
-    vv = (float)(bf16)(vv * beta2);
-    vv = (float)(bf16)(vv + one_m_b2 * g * g);
-    m_lat[e] = (bf16)m;
-    v_lat[e] = (bf16)vv;
-    float den = (float)(bf16)sqrtf(vv);
-    den = (float)(bf16)(den / bc2s);
-    den = (float)(bf16)(den + eps);
     const float x = (float)x8[pix * 8 + 4 + k];
-    const float xp = (float)(bf16)(x + (-step_size) * (m / den));
+    float xp;
+    if (opt == 0) {
+      float m = (float)m_lat[e], vv = (float)v_lat[e];
+      m = (float)(bf16)(m + beta1w * (g - m));
+      vv = (float)(bf16)(vv * beta2);
+      vv = (float)(bf16)(vv + one_m_b2 * g * g);
+      m_lat[e] = (bf16)m;
+      v_lat[e] = (bf16)vv;
+      float den = (float)(bf16)sqrtf(vv);
+      den = (float)(bf16)(den / bc2s);
+      den = (float)(bf16)(den + eps);
+      xp = (float)(bf16)(x + (-step_size) * (m / den));
+    } else if (opt == 1) {
+      xp = (float)(bf16)(x + (-step_size) * g);
+    } else {
+      float sum = (float)(bf16)((float)m_lat[e] + g * g);
+      m_lat[e] = (bf16)sum;
+      const float sd = (float)(bf16)((float)(bf16)sqrtf(sum) + 1e-10f);
+      xp = (float)(bf16)(x + (-step_size) * (g / sd));
+    }
     const float vm = (float)v[pix * 8 + k];
     const float x0 = (float)(bf16)((float)(bf16)(sa * xp) - (float)(bf16)(sb * vm));
     const float ep = (float)(bf16)((float)(bf16)(sa * vm) + (float)(bf16)(sb * xp));
@@ -371,19 +420,27 @@ __global__ void latent_update_kernel(bf16* x8, const bf16* v, const bf16* gdir, 
     x8[pix * 8 + 4 + k] = (bf16)prev;
   }
   if (threadIdx.x < 2) {
-    // Adam on scale (0) / shift (1), fp32
+    // the same rule on scale (0) / shift (1), fp32 state
     const int j = threadIdx.x;
     const float g = daff_grad[n * 2 + j];
-    float m = m_aff[n * 2 + j], vv = v_aff[n * 2 + j];
-    m = m + beta1w * (g - m);
-    vv = vv * beta2;
-    vv = vv + one_m_b2 * g * g;
-    m_aff[n * 2 + j] = m;
-    v_aff[n * 2 + j] = vv;
-    float den = sqrtf(vv);
-    den = den / bc2s;
-    den = den + eps;
-    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (m / den);
+    if (opt == 0) {
+      float m = m_aff[n * 2 + j], vv = v_aff[n * 2 + j];
+      m = m + beta1w * (g - m);
+      vv = vv * beta2;
+      vv = vv + one_m_b2 * g * g;
+      m_aff[n * 2 + j] = m;
+      v_aff[n * 2 + j] = vv;
+      float den = sqrtf(vv);
+      den = den / bc2s;
+      den = den + eps;
+      affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (m / den);
+    } else if (opt == 1) {
+      affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * g;
+    } else {
+      const float sum = m_aff[n * 2 + j] + g * g;
+      m_aff[n * 2 + j] = sum;
+      affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (g / (sqrtf(sum) + 1e-10f));
+    }
   }
   if (dbg && threadIdx.x == 0) {
     dbg[n * 4 + 0] = gn;
@@ -596,11 +653,12 @@ __global__ void sparse_loss_cf_kernel(const bf16* out, int ldo, int PH, int PW, 
 // Per-input training (train_method="per-input", marigold_dc.py:911-967) with learned affine params: the
 // reference's optimiser still holds the pre-loop latent tensor (:777-783 vs :913), so only scale / shift
 // move; the decode A of the final latents is fixed, and each of the train_steps iterations is the l1 + l2
-// loss on the UNclamped s^2 (max - min) A + sh^2 min at the sparse pixels followed by one fp32 Adam step
-// (torch.optim.Adam arithmetic, step count 1..train_steps).  One block per frame, all steps in one launch.
+// loss on the UNclamped s^2 (max - min) A + sh^2 min at the sparse pixels followed by one fp32 optimiser
+// step (opt 0 Adam with step count 1..train_steps, 1 SGD, 2 Adagrad; torch.optim arithmetic).  One block
+// per frame, all steps in one launch.
 __global__ void affine_fit_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
                                   const int* idx, const float* gval, const int* cnt, const float* params,
-                                  int train_steps, float lr, float* affine, float* loss) {
+                                  int train_steps, float lr, int opt, float* affine, float* loss) {
   __shared__ float scratch[16];
   __shared__ float s_aff[2];
   const int n = blockIdx.x;
@@ -651,12 +709,22 @@ __global__ void affine_fit_kernel(const bf16* out, int ldo, int PH, int PW, int 
       const float step_size = (float)(lr / (1.0 - b1p));
       const float bc2s = (float)sqrt(1.0 - b2p);
       const float g0 = db * (gmax - gmin) * (2.0f * s), g1 = (de * gmin) * (2.0f * sh);
-      m0 = m0 + beta1w * (g0 - m0);
-      v0 = v0 * beta2 + one_m_b2 * g0 * g0;
-      m1 = m1 + beta1w * (g1 - m1);
-      v1 = v1 * beta2 + one_m_b2 * g1 * g1;
-      s_aff[0] = s + (-step_size) * (m0 / (sqrtf(v0) / bc2s + eps));
-      s_aff[1] = sh + (-step_size) * (m1 / (sqrtf(v1) / bc2s + eps));
+      if (opt == 0) {
+        m0 = m0 + beta1w * (g0 - m0);
+        v0 = v0 * beta2 + one_m_b2 * g0 * g0;
+        m1 = m1 + beta1w * (g1 - m1);
+        v1 = v1 * beta2 + one_m_b2 * g1 * g1;
+        s_aff[0] = s + (-step_size) * (m0 / (sqrtf(v0) / bc2s + eps));
+        s_aff[1] = sh + (-step_size) * (m1 / (sqrtf(v1) / bc2s + eps));
+      } else if (opt == 1) {
+        s_aff[0] = s + (-lr) * g0;
+        s_aff[1] = sh + (-lr) * g1;
+      } else {  // Adagrad: m0 / m1 hold the squared-gradient sums
+        m0 = m0 + g0 * g0;
+        m1 = m1 + g1 * g1;
+        s_aff[0] = s + (-lr) * (g0 / (sqrtf(m0) + 1e-10f));
+        s_aff[1] = sh + (-lr) * (g1 / (sqrtf(m1) + 1e-10f));
+      }
       loss[n] = ls;
     }
     __syncthreads();
@@ -719,13 +787,14 @@ extern "C" int dc_decode_tail_bwd(const void* dec_out, int ldo, const float* dA,
 extern "C" int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gunet, int nb, int hw,
                                 const float* coef, const float* adam_tab, const int* step, const float* eps_norm,
                                 void* m_lat, void* v_lat, float* affine, float* m_aff, float* v_aff,
-                                const float* daff_grad, float* dbg, void* stream) {
+                                const float* daff_grad, float* dbg, int opt, int kld_mode, float kld_weight,
+                                void* stream) {
   if (!x8 || !v || !gdir || !gunet || !coef || !adam_tab || !step || !eps_norm || !m_lat || !v_lat || !affine ||
-      !m_aff || !v_aff || !daff_grad || nb <= 0 || hw <= 0)
+      !m_aff || !v_aff || !daff_grad || nb <= 0 || hw <= 0 || opt < 0 || opt > 2 || kld_mode < 0 || kld_mode > 2)
     return DC_ERR_ARG;
   hipLaunchKernelGGL(latent_update_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, (bf16*)x8, (const bf16*)v,
                      (const bf16*)gdir, (const bf16*)gunet, hw, coef, adam_tab, step, eps_norm, (bf16*)m_lat,
-                     (bf16*)v_lat, affine, m_aff, v_aff, daff_grad, dbg);
+                     (bf16*)v_lat, affine, m_aff, v_aff, daff_grad, dbg, opt, kld_mode, kld_weight);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -794,12 +863,12 @@ extern "C" int dc_sparse_loss_cf(const void* dec_out, int ldo, int nb, int ph, i
 
 extern "C" int dc_affine_fit(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
                              const int* idx, const float* gval, const int* cnt, const float* params, int train_steps,
-                             float lr, float* affine, float* loss, void* stream) {
+                             float lr, int opt, float* affine, float* loss, void* stream) {
   if (!dec_out || !idx || !gval || !cnt || !params || !affine || !loss || nb <= 0 || train_steps <= 0 ||
-      rh > ph || rw > pw)
+      rh > ph || rw > pw || opt < 0 || opt > 2)
     return DC_ERR_ARG;
   hipLaunchKernelGGL(affine_fit_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
-                     pw, rh, rw, h, w, idx, gval, cnt, params, train_steps, lr, affine, loss);
+                     pw, rh, rw, h, w, idx, gval, cnt, params, train_steps, lr, opt, affine, loss);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

@@ -174,6 +174,7 @@ class MarigoldDepthCompletionPipeline:
         # Modes (marigold_dc.py:758-967), all on the same kernels:
         #  guided    train_latents, per-step: the guided DDIM loop (learned affine, or closed_form=True with
         #            the fit differentiated: dc_sparse_loss_cf)
+        # (optimisers Adam / SGD / Adagrad; the KL term of kld=True joins the latent gradient)
         #  per-input train_latents, per-input: plain DDIM loop, then train_steps optimiser steps which --
         #            as the reference's optimiser holds the pre-loop latent tensor (:777-783 vs :913) -- move
         #            only the learned scale / shift (dc_affine_fit); with closed_form nothing moves at all
@@ -181,17 +182,18 @@ class MarigoldDepthCompletionPipeline:
         guided = train_latents and train_method == "per-step"
         fit_affine = train_latents and train_method == "per-input" and not closed_form
         optimised = guided or fit_affine
+        if kld and kld_mode not in ("simple", "strict"):
+            raise ValueError(f"Unknown mode: {kld_mode}")
+        opt_code = {"adam": 0, "sgd": 1, "adagrad": 2}[opt]
+        # (per-input: the KL term reaches only the latents, which do not move)
+        kld_code = {"simple": 1, "strict": 2}[kld_mode] if (kld and guided) else 0
         unsupported = []
-        if optimised and opt != "adam":
-            unsupported.append(f"opt={opt}")
-        if guided and kld:   # (per-input: the KL term reaches only the latents, which do not move)
-            unsupported.append("kld")
         if optimised and sorted(loss_funcs) != ["l1", "l2"]:
             unsupported.append(f"loss_funcs={loss_funcs}")
         if interp_mode != "bilinear":
             unsupported.append(f"interp_mode={interp_mode}")
         if unsupported:
-            raise NotImplementedError("HIP path supports Adam with the l1 + l2 loss for the optimised modes; got "
+            raise NotImplementedError("HIP path supports the l1 + l2 loss for the optimised modes; got "
                                       + ", ".join(unsupported))
         dev = self.device
         ctx = self.ctx
@@ -248,7 +250,8 @@ class MarigoldDepthCompletionPipeline:
         # ---- per-call tables
         ts = self.scheduler.timesteps(steps)
         coef = self.scheduler.coef(steps).to(dev)
-        adam = adam_table(steps, lr_latent, lr_scaling).to(dev)
+        adam = (adam_table(steps, lr_latent, lr_scaling) if opt == "adam" else
+                torch.tensor([[lr_latent, 0.0, lr_scaling, 0.0]] * steps, dtype=torch.float32)).to(dev)
         self.unet.build_temb_tables(ctx, ts)
         for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"], st["daff"]):
             ops.memset(ctx, t)
@@ -256,13 +259,15 @@ class MarigoldDepthCompletionPipeline:
         ops.memset(ctx, ctx.step)
         cf = bool(closed_form)
         self._call_state = dict(idx=idx, gval=gval, cnt=cnt, params=params, coef=coef, adam=adam, H=H, W=W, RH=RH,
-                                RW=RW, PH=PH, PW=PW, n=n, h=h, w=w, cf=cf)
+                                RW=RW, PH=PH, PW=PW, n=n, h=h, w=w, cf=cf, opt=opt_code, kld=kld_code,
+                                kld_weight=float(kld_weight))
 
         # ---- denoising loop (marigold_dc.py:800-909): guided steps, or plain DDIM steps
         step_fn = self._step if guided else self._ddim_step
         if self.use_graph:
             g = st["graph"]
-            gkey = (guided, guided and cf, steps, H, W, RH, RW, lr_latent, lr_scaling)
+            gkey = (guided, guided and cf, opt_code, kld_code, float(kld_weight), steps, H, W, RH, RW, lr_latent,
+                    lr_scaling)
             if g is None or st["graph_key"] != gkey:
                 # tables are rebuilt per call at new addresses: capture against this call's buffers
                 g = torch.cuda.CUDAGraph()
@@ -298,7 +303,7 @@ class MarigoldDepthCompletionPipeline:
         if fit_affine:   # per-input training of scale / shift on the (fixed) final decode (:911-967)
             _lib.call("dc_affine_fit", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["idx"].data_ptr(),
                       cs["gval"].data_ptr(), cs["cnt"].data_ptr(), cs["params"].data_ptr(), int(train_steps),
-                      float(lr_scaling), st["affine"].data_ptr(), st["loss"].data_ptr(), ctx.stream)
+                      float(lr_scaling), opt_code, st["affine"].data_ptr(), st["loss"].data_ptr(), ctx.stream)
         if closed_form:   # compute_affine_params on the final decode (marigold_dc.py:332-336)
             _lib.call("dc_closed_form_affine", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["idx"].data_ptr(),
                       cs["gval"].data_ptr(), cs["cnt"].data_ptr(), st["affine"].data_ptr(), ctx.stream)
@@ -370,5 +375,6 @@ class MarigoldDepthCompletionPipeline:
         _lib.call("dc_latent_update", up.x8.data_ptr(), up.v.data_ptr(), st["gdir"].data_ptr(), up.gx.data_ptr(), n,
                   h * w, cs["coef"].data_ptr(), cs["adam"].data_ptr(), step, st["eps_norm"].data_ptr(),
                   st["m_lat"].data_ptr(), st["v_lat"].data_ptr(), st["affine"].data_ptr(), st["m_aff"].data_ptr(),
-                  st["v_aff"].data_ptr(), st["daff"].data_ptr(), st["dbg"].data_ptr(), s)
+                  st["v_aff"].data_ptr(), st["daff"].data_ptr(), st["dbg"].data_ptr(), cs["opt"], cs["kld"],
+                  cs["kld_weight"], s)
         _lib.call("dc_step_advance", step, int(cs["coef"].shape[0]), s)

@@ -132,9 +132,12 @@ int dc_sparse_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh,
                    float* daff_grad, float* loss, void* stream);
 int dc_decode_tail_bwd(const void* dec_out, int ldo, const float* dA, int nb, int ph, int pw, int rh, int rw,
                        void* dout, void* stream);
+/* opt: 0 Adam, 1 SGD, 2 Adagrad (marigold_dc.py:783-789); kld_mode: 0 off, 1 "simple", 2 "strict"
+ * (utils.kld_stdnorm), weighted by kld_weight; for SGD / Adagrad adam_tab rows are [lr_lat, 0, lr_aff, 0] */
 int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gunet, int nb, int hw, const float* coef,
                      const float* adam_tab, const int* step, const float* eps_norm, void* m_lat, void* v_lat,
-                     float* affine, float* m_aff, float* v_aff, const float* daff_grad, float* dbg, void* stream);
+                     float* affine, float* m_aff, float* v_aff, const float* daff_grad, float* dbg, int opt,
+                     int kld_mode, float kld_weight, void* stream);
 int dc_step_advance(int* step, int nsteps, void* stream);  /* saturates at nsteps-1 */
 int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8, void* stream);
 int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
@@ -153,8 +156,8 @@ int dc_sparse_loss_cf(const void* dec_out, int ldo, int nb, int ph, int pw, int 
 /* train_method="per-input" with learned affine (marigold_dc.py:911-967): train_steps Adam steps on
  * affine[nb][2] (scale, shift) against the fixed decode of the final latents */
 int dc_affine_fit(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w, const int* idx,
-                  const float* gval, const int* cnt, const float* params, int train_steps, float lr, float* affine,
-                  float* loss, void* stream);
+                  const float* gval, const int* cnt, const float* params, int train_steps, float lr, int opt,
+                  float* affine, float* loss, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
 
 #ifdef __cplusplus

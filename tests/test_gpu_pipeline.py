@@ -221,3 +221,17 @@ def test_guided_depth_space(kw):
 def test_per_input_projected():
     _mode_parity(dict(norm="minmax", projection="log", min_depth=1.0, steps=5, train_method="per-input",
                       train_steps=8), 24, "per-input log")
+
+
+@pytest.mark.parametrize("kw", [dict(opt="sgd", kld=True), dict(opt="adagrad"),
+                                dict(kld=True, kld_mode="strict", kld_weight=0.5),
+                                dict(opt="sgd", lr=(0.5, 0.05))])
+def test_guided_optimisers_kld(kw):
+    """Guided steps with SGD / Adagrad (marigold_dc.py:783-789) and the KL term (utils.py:28-86)."""
+    _mode_parity(dict(kw, norm="const", steps=6), 25, f"guided {kw}", fitted=True)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adagrad"])
+def test_per_input_optimisers(opt):
+    _mode_parity(dict(norm="minmax", steps=5, train_method="per-input", train_steps=10, opt=opt, lr=(0.05, 0.05)),
+                 26, f"per-input {opt}")
