@@ -45,6 +45,21 @@ from oracle.diffusers_ref import (AutoencoderTiny, DDIMScheduler, UNet2DConditio
 from oracle.pipeline_ref import MarigoldBase  # noqa: E402
 
 
+def host_fingerprint() -> str:
+    """CPU kernels (oneDNN bf16 conv, vectorised libm) differ between host ISAs, so the vectors
+    are bit-exact only on a host with the same fingerprint (tests/test_oracle_golden.py)."""
+    flags = set()
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("flags"):
+                flags = set(line.split(":", 1)[1].split())
+                break
+    except OSError:
+        pass
+    isa = [f for f in ("amx_bf16", "avx512_bf16", "avx512f", "avx2") if f in flags]
+    return f"torch {torch.__version__} / {torch.backends.cpu.get_cpu_capability()} / {'+'.join(isa)}"
+
+
 def _extract(path: Path, names: set[str], cls: str | None = None, methods: set[str] | None = None):
     tree = ast.parse(path.read_text())
     funcs, meths = [], []
@@ -188,7 +203,7 @@ def main():
     ns, uns, RefPipeline = load_reference()
     unit = make_unit_vectors(ns, uns)
     save_file(unit, str(HERE / "unit_functions.safetensors"))
-    meta = {"unit_functions": sorted(unit)}
+    meta = {"unit_functions": sorted(unit), "host": host_fingerprint()}
     for name, spec in PIPE_CASES.items():
         out = run_pipe_case(RefPipeline, name, spec)
         save_file(out, str(HERE / f"pipe_{name}.safetensors"))
