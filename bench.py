@@ -7,7 +7,9 @@ data-path collective (scaling = weak); the barrier + max-over-ranks timing is th
 
 Also reported on the same JSON line:
   roofline      the dominant kernel (implicit-GEMM conv/linear, dc_conv_gemm) timed with HIP events
-                on its launch stream during one instrumented step: algorithmic FLOPs / avg duration
+                on its launch stream around each launch of one live (eager) guided step:
+                algorithmic FLOPs / avg duration; `traffic` from the committed PMC pass
+                (profiles/pmc_conv_gemm.json, FETCH_SIZE x2 + WRITE_SIZE per launch, gfx950 correction)
   cpu_baseline  the oracle (CPU PyTorch restatement of the reference path, incl. weight-gradients as
                 the reference computes them) on this host's cores, rank 0 / N=1 only, on a bounded
                 sample (1- and 2-step calls, extrapolated to 50 steps)
@@ -54,51 +56,41 @@ def conv_flops(d) -> float:
     return f
 
 
-def measure_conv_kernel(pipe, st, reps: int = 10):
-    """Average duration of the dominant kernel (dc_conv_gemm) over one guided step.
+def measure_conv_kernel(pipe, st):
+    """Average duration of the dominant kernel (dc_conv_gemm) over one live guided step.
 
-    The step's conv launches are recorded from one eager step (their descriptors copied); each is
-    then captured `reps` times back-to-back into a small hipGraph and replayed between two HIP
-    events on the launch stream, so the events bracket GPU execution only (no host launch gaps).
-    Returns (launches, summed avg duration ms, algorithmic FLOPs) for one step.
+    One eager step of the pipeline runs with a pair of HIP events recorded on the launch stream
+    around every dc_conv_gemm launch, in the step's own order and cache state (no replays); the
+    events bracket each launch's GPU execution.  Returns (launches, summed duration ms, algorithmic
+    FLOPs) for the step.
     """
-    import ctypes as C
-
-    from depth_completion_amd import _lib, ops
+    from depth_completion_amd import ops
     from depth_completion_amd._lib import ConvDesc
-    descs = []
+    marks = []
     orig = ops.call
 
-    def recorder(name, *args):
-        if name == "dc_conv_gemm":
-            descs.append(ConvDesc.from_buffer_copy(args[0]._obj))
-        return orig(name, *args)
+    def timed(name, *args):
+        if name != "dc_conv_gemm":
+            return orig(name, *args)
+        stream = torch.cuda.current_stream()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r = orig(name, *args)
+        e1.record(stream)
+        marks.append((e0, e1, ConvDesc.from_buffer_copy(args[0]._obj)))
+        return r
 
-    ops.call = recorder
+    ops.call = timed
     try:
         ops.memset(pipe.ctx, pipe.ctx.step)  # step index 0: per-step tables have exactly S rows
         pipe._step(st)
     finally:
         ops.call = orig
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    total_ms, flops = 0.0, 0.0
-    for d in descs:
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for _ in range(reps):
-                _lib.call("dc_conv_gemm", C.byref(d), torch.cuda.current_stream().cuda_stream)
-        g.replay()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        g.replay()
-        e1.record(stream)
-        e1.synchronize()
-        total_ms += e0.elapsed_time(e1) / reps
-        flops += conv_flops(d)
-        del g
-    return len(descs), total_ms, flops
+    total_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in marks)
+    flops = sum(conv_flops(d) for _, _, d in marks)
+    return len(marks), total_ms, flops
 
 
 def cpu_baseline(h, w, n_points):
@@ -192,8 +184,14 @@ def main():
     n_launch, conv_ms, conv_flops_ = measure_conv_kernel(pipe, st)
     avg_ms = conv_ms / max(n_launch, 1)
     achieved = conv_flops_ / (conv_ms * 1e-3) / 1e12
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_conv_gemm.json")
+    if B == 1 and os.path.exists(pmc):   # committed PMC pass of the C2 step (tools/pmc_traffic.py)
+        with open(pmc) as f:
+            traffic = round(json.load(f)["traffic_bytes_per_launch"])
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, C2 step)",
                 "kernel": "dc_conv_gemm = conv_gemm_kernel (split-K partials reduced in-kernel by the last block), implicit-GEMM conv/linear",
                 "launches_per_step": n_launch, "avg_launch_ms": round(avg_ms, 5),
                 "algorithmic_gflop_per_step": round(conv_flops_ / 1e9, 1)}

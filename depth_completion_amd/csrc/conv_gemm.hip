@@ -12,8 +12,10 @@
 // and tails read a zero line), XOR-swizzled through the source permutation so the ds_read_b128
 // fragment reads are conflict-free; S-2 k-chunks stay in flight across the (raw) barrier under a
 // counted vmcnt.  The epilogue stages the fp32 tile through LDS and applies bias / per-step row bias
-// (time embedding) / residual / ReLU / ReLU-backward mask with 16-B coalesced accesses.  Split-K
-// writes fp32 partial slabs that a second kernel reduces through the same epilogue.
+// (time embedding) / residual / ReLU / ReLU-backward mask with 16-B coalesced accesses.  Work
+// decomposition: plain tiles, split-K, or stream-K (equal contiguous ranges of the tile x k-chunk
+// iteration space per block); a tile computed in pieces is summed in piece order by its
+// last-arriving block (deterministic, no second kernel).
 #include <type_traits>
 
 #include "common.h"
@@ -42,8 +44,9 @@ struct ConvGemmParams {
   int ldy;
   float* ws;            // split-K partial slabs [splits][tiles][BM*BN]; tile counters in the last 64 KB
   long ws_bytes;
-  int splits, kps;
+  int splits, kps;       // split-K: splits, k-chunks per split; stream-K: tile count, nk
   int* counters;        // [tiles] arrival counts, zero between launches (the workspace starts zeroed)
+  int sk_blocks;        // > 0: stream-K over this many blocks (split-K / plain tiles: 0)
 };
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of every padded / out-of-range piece
@@ -161,8 +164,12 @@ __device__ __forceinline__ int swz(int row) {
   else return ((row >> 3) & 1) << 1;
 }
 
+// Mainloop of one (tile, k-range) segment: gathers A / W chunks [kc_begin, kc_end) through the LDS ring
+// and accumulates into acc (zeroed here).  Ends with every LDS-DMA landed; the ring is still being read
+// by other waves until the caller's next barrier.
 template <int BM, int BN, int BK, int S, bool SMALLC>
-__global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) {
+__device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, long m0, int n0, int kc_begin,
+                                          int kc_end, f32x4 (&acc)[BM / 32][BN / 32]) {
   constexpr int CPR = BK / 8;            // 16-B chunks per tile row
   constexpr int RPI = 256 / CPR;         // tile rows covered by one block-wide LDS-DMA instruction
   constexpr int AP = BM / RPI;           // A pieces (16 B) per thread per k-chunk
@@ -174,29 +181,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   constexpr int MI = WM / 16, NJ = WN / 16;
   constexpr int STAGE = Cfg<BM, BN, BK, S>::STAGE;
   static_assert(AP >= 1 && BP >= 1, "tile too small for the block-wide DMA");
-  __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, BK, S>::LDS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const long hwo = (long)p.hout * p.wout;
   const long M = (long)p.nb * hwo;
-  const int tiles_n = (p.cout + BN - 1) / BN;
-
-  // bijective XCD-aware remap over the whole (tile, split) grid: workgroups are dealt round-robin to
-  // the 8 XCDs by linear id, so XCD x = id % 8 gets the contiguous work range x * total / 8 ... in
-  // split-major order -- with K split 8 ways each XCD streams one K slice of A and W through its own L2
-  // (each byte fetched from HBM once); unsplit, each XCD gets a contiguous run of row tiles.
-  const int tiles = gridDim.x, nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
-  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  const int wk = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int split = wk / tiles, lb = wk - split * tiles;
-  const int tm = lb / tiles_n, tn = lb - tm * tiles_n;
-  const long m0 = (long)tm * BM;
-  const int n0 = tn * BN;
-
-  const int nk = p.ktot / BK;
-  const int kc_begin = split * p.kps;
-  const int kc_end = min(nk, kc_begin + p.kps);
   const int nkc = max(0, kc_end - kc_begin);
 
   // per-thread A-row gather tables (piece j covers tile row tid/CPR + RPI j, chunk slot tid%CPR):
@@ -362,7 +351,6 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     }
   };
 
-  f32x4 acc[MI][NJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -405,58 +393,74 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     __builtin_amdgcn_sched_group_barrier(0x008, KS * MI * NJ, 0);
   }
   vm_wait<0>();
+}
 
-  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  if (p.splits > 1) {
-    // split-K, reduced in-kernel by the tile's last-arriving block (deterministic: partials are summed
-    // in split order).  Partials go out in the accumulator-native layout [split][tile][wave][i][j][lane]
-    // as 16-B sc1 stores; one lane per block then bumps the tile's counter (agent-scope atomic) after
-    // every wave's vmcnt(0); the block that sees splits-1 reads the others back with sc1 loads
-    // (MI355X_MICROARCH.md hand-off table, row 1) and runs the normal epilogue.
-    constexpr int TILE_F = BM * BN;
-    const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
-    const long slab = ((long)split * gridDim.x + lb) * TILE_F + wid * (WM * WN) + lane * 4;
+// Partial-sum hand-off of a tile computed in `narrive` k-segments (deterministic: the tile's
+// last-arriving block sums every segment's partial in segment order).  Partials go out in the
+// accumulator-native layout [slot][wave][i][j][lane] as 16-B sc1 stores; one lane per block then bumps
+// the tile's counter (agent-scope atomic) after every wave's vmcnt(0); the block that arrives last reads
+// all partials back with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1), leaves their sum in acc
+// and returns true (the caller then runs the epilogue).  slot_of(i) = slab slot of segment i.
+template <int BM, int BN, typename SlotFn>
+__device__ __forceinline__ bool tile_handoff(const ConvGemmParams& p, char* smem, int tile, int my_slot, int narrive,
+                                             SlotFn slot_of, f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int MI = WM / 16, NJ = WN / 16;
+  constexpr int TILE_F = BM * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
+  const long slab = (long)my_slot * TILE_F + wid * (WM * WN) + lane * 4;
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) store_sc1_x4(rs, slab + (i * NJ + j) * 256, acc[i][j]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the flag lives in the (now idle) ring: a second __shared__ object would make the compiler's
-    // waitcnt pass treat every LDS-DMA as aliasing the main loop's ds_reads (vmcnt(0) per chunk)
-    int* s_last = reinterpret_cast<int*>(smem);
-    __syncthreads();
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(p.counters + lb, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *s_last = old == p.splits - 1;
-    }
-    __syncthreads();
-    if (!*s_last) return;
-    // every split's partial (this block's own included) is read back in split order
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // (in row halves of the wave tile, to keep the register peak of the main loop's occupancy)
-    constexpr int MH = MI > 1 ? MI / 2 : 1;
-#pragma unroll
-    for (int i0 = 0; i0 < MI; i0 += MH) {
-      for (int sp = 0; sp < p.splits; ++sp) {
-        const long src = ((long)sp * gridDim.x + lb) * TILE_F + wid * (WM * WN) + lane * 4;
-        f32x4 part[MH][NJ];
-#pragma unroll
-        for (int i = 0; i < MH; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) part[i][j] = load_sc1_x4(rs, src + ((i0 + i) * NJ + j) * 256);
-#pragma unroll
-        for (int i = 0; i < MH; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i0 + i][j] += part[i][j];
-      }
-    }
-    if (tid == 0) p.counters[lb] = 0;  // ready for the next launch (ordered by the kernel boundary)
+    for (int j = 0; j < NJ; ++j) store_sc1_x4(rs, slab + (i * NJ + j) * 256, acc[i][j]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the flag lives in the (now idle) ring: a second __shared__ object would make the compiler's
+  // waitcnt pass treat every LDS-DMA as aliasing the main loop's ds_reads (vmcnt(0) per chunk)
+  int* s_last = reinterpret_cast<int*>(smem);
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_last = old == narrive - 1;
   }
+  __syncthreads();
+  if (!*s_last) return false;
+  // every segment's partial (this block's own included) is read back in segment order
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // (in row halves of the wave tile, to keep the register peak of the main loop's occupancy)
+  constexpr int MH = MI > 1 ? MI / 2 : 1;
+#pragma unroll
+  for (int i0 = 0; i0 < MI; i0 += MH) {
+    for (int sp = 0; sp < narrive; ++sp) {
+      const long src = (long)slot_of(sp) * TILE_F + wid * (WM * WN) + lane * 4;
+      f32x4 part[MH][NJ];
+#pragma unroll
+      for (int i = 0; i < MH; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) part[i][j] = load_sc1_x4(rs, src + ((i0 + i) * NJ + j) * 256);
+#pragma unroll
+      for (int i = 0; i < MH; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i0 + i][j] += part[i][j];
+    }
+  }
+  if (tid == 0) p.counters[tile] = 0;  // ready for the next launch (ordered by the kernel boundary)
+  return true;
+}
 
-  // ---- epilogue: bias in fp32, round to bf16 into a per-wave LDS tile, then 16-B coalesced rows
+// epilogue: bias in fp32, round to bf16 into a per-wave LDS tile, then 16-B coalesced rows
+template <int BM, int BN>
+__device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* smem, long m0, int n0,
+                                              const f32x4 (&acc)[BM / 32][BN / 32]) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int MI = WM / 16, NJ = WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const long M = (long)p.nb * p.hout * p.wout;
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   __syncthreads();  // every wave is done reading the ring
   constexpr int LDE = WN + 8;
   bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
@@ -484,6 +488,75 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   }
 }
 
+// bijective XCD-aware remap of a linear block id: workgroups are dealt round-robin to the 8 XCDs by
+// linear id, so XCD x = id % 8 gets the contiguous logical range x * total / 8 ...
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int BM, int BN, int BK, int S, bool SMALLC>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, BK, S>::LDS];
+  f32x4 acc[BM / 32][BN / 32];
+  const int tiles_n = (p.cout + BN - 1) / BN;
+  const int nk = p.ktot / BK;
+
+  if (p.sk_blocks == 0) {
+    // split-K (splits == 1: plain tiles).  Split-major logical order over the whole (tile, split)
+    // grid: with K split 8 ways each XCD streams one K slice of A and W through its own L2 (each byte
+    // fetched from HBM once); unsplit, each XCD gets a contiguous run of row tiles.
+    const int tiles = gridDim.x, nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int wk = xcd_remap(bid, nblk);
+    const int split = wk / tiles, lb = wk - split * tiles;
+    const int tm = lb / tiles_n, tn = lb - tm * tiles_n;
+    const long m0 = (long)tm * BM;
+    const int n0 = tn * BN;
+    const int kc_begin = split * p.kps;
+    const int kc_end = min(nk, kc_begin + p.kps);
+    tile_pass<BM, BN, BK, S, SMALLC>(p, smem, m0, n0, kc_begin, kc_end, acc);
+    if (p.splits > 1 &&
+        !tile_handoff<BM, BN>(p, smem, lb, split * tiles + lb, p.splits, [&](int sp) { return sp * tiles + lb; },
+                              acc))
+      return;
+    tile_epilogue<BM, BN>(p, smem, m0, n0, acc);
+    return;
+  }
+
+  // stream-K: the tiles x nk k-chunk iterations are dealt out as G equal contiguous ranges (logical
+  // block b gets [b U / G, (b + 1) U / G)), so every block does the same MFMA work whatever the tile
+  // count; a tile cut between blocks is finished by its last-arriving block (tile_handoff).  Slab
+  // slots: 2b for block b's first segment, 2b + 1 for its last.
+  const int G = gridDim.x;
+  const long U = (long)p.splits * nk;  // p.splits carries the tile count in stream-K mode
+  const int b = xcd_remap(blockIdx.x, G);
+  long it = (long)b * U / G;
+  const long start = it, end = (long)(b + 1) * U / G;
+  // logical block holding iteration i: the largest b with b U / G <= i
+  auto owner = [&](long i) { return (int)(((i + 1) * G - 1) / U); };
+  while (it < end) {
+    const int tile = (int)(it / nk);
+    const int kb = (int)(it - (long)tile * nk);
+    const int ke = (int)min((long)nk, kb + (end - it));
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const long m0 = (long)tm * BM;
+    const int n0 = tn * BN;
+    tile_pass<BM, BN, BK, S, SMALLC>(p, smem, m0, n0, kb, ke, acc);
+    bool mine = true;
+    if (kb != 0 || ke != nk) {
+      const long t0 = (long)tile * nk;
+      const int bf = owner(t0), bl = owner(t0 + nk - 1);
+      const int slot = (it == start) ? 2 * b : 2 * b + 1;
+      mine = tile_handoff<BM, BN>(
+          p, smem, tile, slot, bl - bf + 1,
+          [&](int i) { const int bb = bf + i; return ((long)bb * U / G >= t0) ? 2 * bb : 2 * bb + 1; }, acc);
+    }
+    if (mine) tile_epilogue<BM, BN>(p, smem, m0, n0, acc);
+    it += ke - kb;
+    __syncthreads();  // the ring / epilogue tile is free before the next segment's LDS-DMA
+  }
+}
+
 constexpr long kCounterBytes = 64 * 1024;
 constexpr int kMaxSplitTiles = (int)(kCounterBytes / 4);
 
@@ -502,13 +575,31 @@ template <int BM, int BN, int BK, int S>
 int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t stream) {
   const int tiles = (int)((M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
   const int nk = p.ktot / BK;
+  p.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(p.ws) + (p.ws_bytes - kCounterBytes));
+  if (splits < 0) {
+    // stream-K over -splits x 256 blocks (at most one per k-chunk iteration; two slab slots per block)
+    long g = min((long)(-splits) * 256, (long)tiles * nk);
+    while (g > 1 && 2 * g * BM * BN * 4 > p.ws_bytes - kCounterBytes) g -= 256 > g ? 1 : 256;
+    if (p.ws != nullptr && tiles <= kMaxSplitTiles && g > 1) {
+      p.sk_blocks = (int)g;
+      p.splits = tiles;
+      p.kps = nk;
+      if (smallc)
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true>), dim3((int)g), dim3(256), 0, stream, p);
+      else
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, false>), dim3((int)g), dim3(256), 0, stream, p);
+      DC_CHECK_LAUNCH();
+      return DC_OK;
+    }
+    splits = 1;
+  }
+  p.sk_blocks = 0;
   splits = max(1, min(splits, nk));
   if (p.ws == nullptr || tiles > kMaxSplitTiles) splits = 1;
   while (splits > 1 && (long)splits * tiles * BM * BN * 4 > p.ws_bytes - kCounterBytes) --splits;
   p.kps = (nk + splits - 1) / splits;
   splits = (nk + p.kps - 1) / p.kps;
   p.splits = splits;
-  p.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(p.ws) + (p.ws_bytes - kCounterBytes));
   if (smallc)
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true>), dim3(tiles, splits), dim3(256), 0, stream, p);
   else
@@ -560,14 +651,14 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   p.y = (bf16*)d->y; p.ldy = d->ldy;
   p.ws = d->ws;
   p.ws_bytes = d->ws_bytes < (1L << 31) ? d->ws_bytes : (1L << 31);  // 32-bit buffer offsets
-  p.splits = 1; p.kps = 0; p.counters = nullptr;
+  p.splits = 1; p.kps = 0; p.counters = nullptr; p.sk_blocks = 0;
   // shape / alignment contract (host pads channels, see DESIGN.md "layouts")
   if (p.ktot % 64 != 0 || p.ktot < p.kh * p.kw * p.cin) return DC_ERR_ARG;
   if (p.cin % 8 != 0 || p.cout <= 0 || p.nb <= 0 || p.hout <= 0 || p.wout <= 0) return DC_ERR_ARG;
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
-  if (d->algo < 0 || d->algo > kNumAlgos || d->splitk < 0) return DC_ERR_ARG;
+  if (d->algo < 0 || d->algo > kNumAlgos || d->splitk < -4) return DC_ERR_ARG;
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;

@@ -156,7 +156,8 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3) -> tuple:
     dt = ConvDesc.from_buffer_copy(d)
     dt.y = tmp.data_ptr() + (d.y - base)
     nalg = _lib.load().dc_conv_num_algos()
-    cands = [(0, 0)] + [(a, s) for a in range(1, nalg + 1) for s in (1, 2, 4, 8, 12, 16, 24, 32)]
+    # split-K 1..32, and stream-K over 256 / 512 / 768 blocks (splitk -1 / -2 / -3)
+    cands = [(0, 0)] + [(a, s) for a in range(1, nalg + 1) for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
     best, best_t = (0, 0), float("inf")
     # DC_TUNE_COLD=1: every timed call starts with L2 and the Infinity Cache flushed (a 512 MiB write),
     # as the weights are in the sampler step (each is touched once per pass)

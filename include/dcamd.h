@@ -53,7 +53,7 @@ typedef struct dc_conv_desc {
   float* ws;       /* split-K workspace (may be NULL: no split-K) */
   long long ws_bytes;
   int algo;        /* 0 = heuristic, 1..dc_conv_num_algos(): tile/ring variant (plan-time autotuned) */
-  int splitk;      /* 0 = heuristic, >=1 explicit K split (needs ws) */
+  int splitk;      /* 0 = heuristic, >=1 explicit K split, -1..-4 stream-K over 256..1024 blocks (needs ws) */
 } dc_conv_desc;
 
 int dc_conv_num_algos(void);

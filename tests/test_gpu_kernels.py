@@ -324,9 +324,11 @@ def test_geglu_and_upsample_adjoint(ctx):
 
 
 @pytest.mark.parametrize("algo", list(range(1, 19)))
-@pytest.mark.parametrize("nsplit", [1, 3])
+@pytest.mark.parametrize("nsplit", [1, 3, -1, -2])
 def test_conv_all_algos(ctx, algo, nsplit):
-    """every tile / ring variant and split-K on conv (incl. concat, stride 2, upsample) and linear."""
+    """every tile / ring variant, split-K (nsplit > 1) and stream-K (nsplit < 0: 256 / 512 blocks over
+    the tile x k-chunk iterations, tiles cut between blocks) on conv (incl. concat, stride 2, upsample)
+    and linear."""
     from depth_completion_amd import ops
     from depth_completion_amd.weights import pack_conv
     cases = [(2, 128, 64, 192, 9, 10, 1, 0), (1, 64, 0, 128, 12, 8, 2, 0), (1, 64, 0, 64, 5, 7, 1, 1),
@@ -350,3 +352,27 @@ def test_conv_all_algos(ctx, algo, nsplit):
                       x2=nhwc(xb) if c2 else None, c1=c1 if c2 else 0, y=y, algo=algo, nsplit=nsplit)
         torch.cuda.synchronize()
         assert rel(nchw(y, n, ho, wo), ref) < 1e-2, (algo, nsplit, n, cin, cout, h, w, stride, mode)
+
+
+@pytest.mark.parametrize("algo,nsplit", [(10, -1), (12, -2), (3, -3), (16, -1)])
+def test_conv_stream_k_unet_shape_deterministic(ctx, algo, nsplit):
+    """stream-K on a UNet L2 shape (M = 432, 3x3, 1280 -> 1280, bias + in-place residual): matches the
+    plain-tile launch within bf16 rounding and is bitwise reproducible run to run."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    n, c, h, w = 1, 1280, 18, 24
+    x = rnd(n, c, h, w, seed=50)
+    wt = rnd(c, c, 3, 3, scale=1 / math.sqrt(c * 9), seed=51)
+    bias = rnd(c, seed=52).contiguous()
+    res = rnd(n, c, h, w, seed=53)
+    ref = F.conv2d(x, wt, bias=bias, padding=1) + res
+    wp = pack_conv(wt).to(dev, torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        y = nhwc(res)
+        ops.conv_gemm(ctx, nhwc(x), wp, nb=n, hin=h, win=w, cin=c, hout=h, wout=w, cout=c, bias=bias, resid=y,
+                      y=y, algo=algo, nsplit=nsplit)
+        torch.cuda.synchronize()
+        outs.append(y.clone())
+    assert rel(nchw(outs[0], n, h, w), ref) < 1e-2
+    assert torch.equal(outs[0], outs[1])

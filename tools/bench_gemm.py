@@ -20,6 +20,8 @@ NALG = _lib.load().dc_conv_num_algos()
 # (name, nb, h, w, cin, cout, k, stride, mode)
 SHAPES = [
     ("big4096_linear", 1, 1, 4096, 4096, 4096, 1, 1, 0),
+    ("L0_proj320", 1, 1, 6912, 320, 320, 1, 1, 0),
+    ("L2_proj1280", 1, 1, 432, 1280, 1280, 1, 1, 0),
     ("L0_conv320", 1, 72, 96, 320, 320, 3, 1, 0),
     ("L0_conv640in", 1, 72, 96, 640, 320, 3, 1, 0),
     ("L1_conv640", 1, 36, 48, 640, 640, 3, 1, 0),
@@ -56,7 +58,7 @@ def main():
 
         flops = 2.0 * nb * ho * wo * cout * k * k * cin
         res = []
-        for algo, ns in [(0, 0)] + [(a, s) for a in range(1, NALG + 1) for s in (1, 2, 4, 8, 16)]:
+        for algo, ns in [(0, 0)] + [(a, s) for a in range(1, NALG + 1) for s in (1, 2, 4, 8, 16, -1, -2, -3)]:
             def run():
                 ops.conv_gemm(ctx, x, wt, nb=nb, hin=hin, win=win, cin=cin, hout=ho, wout=wo, cout=cout, kh=k,
                               kw=k, stride=stride, pad=k // 2, mode=mode, bias=b, y=y, algo=algo, nsplit=ns)
@@ -73,10 +75,12 @@ def main():
             ms = e0.elapsed_time(e1) / args.reps
             res.append((ms, algo, ns))
         auto_ms = res[0][0]
-        best = min(res)
+        best = min(r for r in res if r[2] >= 0)
+        bsk = min(r for r in res if r[2] < 0)
         print(f"{name:18s} M={nb*ho*wo:7d} N={cout:6d} K={k*k*cin:6d}  auto {auto_ms*1e3:8.1f} us "
-              f"{flops/auto_ms/1e9:7.1f} TF | best algo {best[1]} split {best[2]} {best[0]*1e3:8.1f} us "
-              f"{flops/best[0]/1e9:7.1f} TF", flush=True)
+              f"{flops/auto_ms/1e9:7.1f} TF | best split-K algo {best[1]} split {best[2]} {best[0]*1e3:8.1f} us "
+              f"{flops/best[0]/1e9:7.1f} TF | best stream-K algo {bsk[1]} G {-bsk[2] * 256} {bsk[0]*1e3:8.1f} us "
+              f"{flops/bsk[0]/1e9:7.1f} TF", flush=True)
 
 
 if __name__ == "__main__":
