@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -60,7 +60,7 @@ _SIGS = {
     "dc_preprocess_image": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp],
     "dc_nhwc_to_nchw": [vp, i32, i32, i64, i32, vp, vp],
     "dc_nchw_to_nhwc": [vp, i32, i64, i32, vp, i32, vp],
-    "dc_sparse_setup": [vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, vp, vp, vp, vp, vp],
+    "dc_sparse_setup": [vp, i32, i32, i32, i32, f32, f32, vp, i32, i32, i32, vp, vp, vp, vp, vp],
     "dc_preview": [vp, vp, i32, i32, vp, vp, vp, vp, vp, vp],
     "dc_sparse_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dc_decode_tail_bwd": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp],
@@ -69,12 +69,15 @@ _SIGS = {
     "dc_latent_init": [vp, vp, f32, i32, i32, vp, vp],
     "dc_final_dense": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp],
     "dc_ddim_step": [vp, vp, i32, i32, vp, vp, vp],
-    "dc_closed_form_affine": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp],
+    "dc_closed_form_affine": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
     "dc_sparse_loss_cf": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp],
     "dc_affine_fit": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, f32, i32, vp, vp, vp],
+    "dc_dense_loss_ws_bytes": [i32, i32, i32],
+    "dc_guide_map": [vp, vp, vp, i32, i32, i32, vp, vp],
+    "dc_dense_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],
 }
-_RESTYPE = {"dc_groupnorm_ws_bytes": i64}
+_RESTYPE = {"dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64}
 
 STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}
 

@@ -495,14 +495,16 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int BM, int BN, int BK, int S, bool SMALLC>
+// SK: stream-K decomposition (its own instantiation: the segment loop's state would otherwise raise the
+// register count -- and cut the occupancy -- of the plain / split-K kernel)
+template <int BM, int BN, int BK, int S, bool SMALLC, bool SK>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, BK, S>::LDS];
   f32x4 acc[BM / 32][BN / 32];
   const int tiles_n = (p.cout + BN - 1) / BN;
   const int nk = p.ktot / BK;
 
-  if (p.sk_blocks == 0) {
+  if constexpr (!SK) {
     // split-K (splits == 1: plain tiles).  Split-major logical order over the whole (tile, split)
     // grid: with K split 8 ways each XCD streams one K slice of A and W through its own L2 (each byte
     // fetched from HBM once); unsplit, each XCD gets a contiguous run of row tiles.
@@ -520,9 +522,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
                               acc))
       return;
     tile_epilogue<BM, BN>(p, smem, m0, n0, acc);
-    return;
-  }
-
+  } else {
   // stream-K: the tiles x nk k-chunk iterations are dealt out as G equal contiguous ranges (logical
   // block b gets [b U / G, (b + 1) U / G)), so every block does the same MFMA work whatever the tile
   // count; a tile cut between blocks is finished by its last-arriving block (tile_handoff).  Slab
@@ -555,6 +555,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     it += ke - kb;
     __syncthreads();  // the ring / epilogue tile is free before the next segment's LDS-DMA
   }
+  }
 }
 
 constexpr long kCounterBytes = 64 * 1024;
@@ -585,9 +586,9 @@ int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t 
       p.splits = tiles;
       p.kps = nk;
       if (smallc)
-        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true>), dim3((int)g), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true, true>), dim3((int)g), dim3(256), 0, stream, p);
       else
-        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, false>), dim3((int)g), dim3(256), 0, stream, p);
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, false, true>), dim3((int)g), dim3(256), 0, stream, p);
       DC_CHECK_LAUNCH();
       return DC_OK;
     }
@@ -601,9 +602,9 @@ int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t 
   splits = (nk + p.kps - 1) / p.kps;
   p.splits = splits;
   if (smallc)
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true>), dim3(tiles, splits), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, true, false>), dim3(tiles, splits), dim3(256), 0, stream, p);
   else
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, false>), dim3(tiles, splits), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, BK, S, false, false>), dim3(tiles, splits), dim3(256), 0, stream, p);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

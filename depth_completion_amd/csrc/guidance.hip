@@ -43,10 +43,10 @@ __device__ float block_min(float v, float* scratch) {
 __device__ float block_max(float v, float* scratch) { return -block_min(-v, scratch); }
 
 // params per frame: [0]=lo [1]=hi (metres) [2]=lo_p [3]=hi_p [4]=min_g [5]=max_g [6]=count
-// [7]=projection + 4 inv (the depth space the loss compares in)
+// [7]=projection + 4 inv (the depth space the loss compares in) + 8 nearest (interp_mode)
 __global__ void sparse_setup_kernel(const float* sparse, int H, int W, int norm, float min_depth, float max_depth,
-                                    const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt,
-                                    float* params) {
+                                    const float* host_lohi, int projection, int inv, int interp, int* idx, float* gval,
+                                    int* cnt, float* params) {
   __shared__ int wave_counts[SETUP_THREADS / 64];
   __shared__ float scratch[SETUP_THREADS / 64];
   __shared__ int base_sh;
@@ -124,7 +124,8 @@ __global__ void sparse_setup_kernel(const float* sparse, int H, int W, int norm,
     cnt[n] = count;
     float* pr = params + n * 8;
     pr[0] = lo; pr[1] = hi; pr[2] = lo_p; pr[3] = hi_p; pr[4] = gmin; pr[5] = gmax;
-    pr[6] = (float)count; pr[7] = (float)(projection + 4 * inv);  // the loss's depth space (DSpace)
+    // the loss's depth space (DSpace) and the resize's interpolation (sample_affine)
+    pr[6] = (float)count; pr[7] = (float)(projection + 4 * inv + 8 * interp);
   }
 }
 
@@ -192,9 +193,29 @@ __device__ __forceinline__ Taps bilinear_taps(int y, int x, int RH, int RW, int 
   return t;
 }
 
+// upsample_nearest2d source index (torch: identity at equal size, >> 1 at exactly 2x, else
+// min(floor(dst * (in / out)), in - 1) in fp32)
+__device__ __forceinline__ int nearest_src(int dst, int in, int out) {
+  if (in == out) return dst;
+  if (out == 2 * in) return dst >> 1;
+  const float scale = (float)in / (float)out;
+  const int s = (int)floorf((float)dst * scale);
+  return s < in - 1 ? s : in - 1;
+}
+
+// interpolation of _latent_to_affine's resize (marigold_dc.py:366-370): params[7] bit 3 = nearest
+__device__ __forceinline__ int interp_nearest(const float* pr) { return ((int)pr[7] >> 3) & 1; }
+
 __device__ __forceinline__ float sample_affine(const bf16* out, int ldo, int n, int PH, int PW, int RH, int RW, int H,
-                                               int W, int y, int x, Taps& t) {
+                                               int W, int y, int x, Taps& t, int nearest) {
   const long base = (long)n * PH * PW;
+  if (nearest) {
+    t.y0 = t.y1 = nearest_src(y, RH, H);
+    t.x0 = t.x1 = nearest_src(x, RW, W);
+    t.ly0 = t.lx0 = 1.0f;
+    t.ly1 = t.lx1 = 0.0f;
+    return decode_tail(out, ldo, base + (long)t.y0 * PW + t.x0);
+  }
   if (RH == H && RW == W) {
     t.y0 = t.y1 = y;
     t.x0 = t.x1 = x;
@@ -220,7 +241,7 @@ struct DSpace {
   __device__ explicit DSpace(const float* pr) {
     const int code = (int)pr[7];
     proj = code & 3;
-    inv = code >> 2;
+    inv = (code >> 2) & 1;
     lo = pr[0]; hi = pr[1]; lo_p = pr[2]; hi_p = pr[3];
   }
   __device__ float operator()(float G, float& dNdG) const {
@@ -263,7 +284,7 @@ __global__ void sparse_loss_kernel(const bf16* out, int ldo, int PH, int PW, int
     const int p = idx[n * HW + k];
     const int y = p / W, x = p - (p / W) * W;
     Taps t;
-    const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t);
+    const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t, interp_nearest(pr));
     const float F = B * aff + E;
     float dNdG;
     const float Nv = ds(fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
@@ -483,8 +504,8 @@ __global__ void final_dense_kernel(const bf16* out, int ldo, int nb, int PH, int
     const int y = (int)((i / W) % H);
     const int n = (int)(i / ((long)H * W));
     Taps t;
-    const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t);
     const float* pr = params + n * 8;
+    const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t, interp_nearest(pr));
     const float s = affine[n * 2], sh = affine[n * 2 + 1];
     float F;
     if (mode == 0) {
@@ -519,17 +540,19 @@ __global__ void ddim_step_kernel(bf16* x8, const bf16* v, long total, const floa
 // one block per frame, with the reference's dtype placement: the affine map is bf16, so its masked sum,
 // mean, centred values, squares and variance are bf16-rounded; guides and the covariance are fp32.
 __global__ void closed_form_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
-                                   const int* idx, const float* gval, const int* cnt, float* affine) {
+                                   const int* idx, const float* gval, const int* cnt, const float* params,
+                                   float* affine) {
   __shared__ float scratch[16];
   const int n = blockIdx.x;
   const long HW = (long)H * W;
   const int count = cnt[n];
   const int* ix = idx + n * HW;
   const float* gv = gval + n * HW;
+  const int nearest = interp_nearest(params + n * 8);
   auto aff_at = [&](int k) {
     const int p = ix[k];
     Taps t;
-    return sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t);
+    return sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t, nearest);
   };
   float sa = 0.0f, sg = 0.0f;
   for (int k = threadIdx.x; k < count; k += blockDim.x) {
@@ -573,9 +596,10 @@ __global__ void sparse_loss_cf_kernel(const bf16* out, int ldo, int PH, int PW, 
   const int count = cnt[n];
   const int* ix = idx + n * HW;
   const float* gv = gval + n * HW;
+  const int nearest = interp_nearest(params + n * 8);
   auto aff_at = [&](int k, Taps& t) {
     const int p = ix[k];
-    return sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t);
+    return sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t, nearest);
   };
   float sa = 0.0f, sg = 0.0f;
   for (int k = threadIdx.x; k < count; k += blockDim.x) {
@@ -686,7 +710,7 @@ __global__ void affine_fit_kernel(const bf16* out, int ldo, int PH, int PW, int 
     for (int k = threadIdx.x; k < count; k += blockDim.x) {
       const int p = ix[k];
       Taps t;
-      const float a = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t);
+      const float a = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t, interp_nearest(pr));
       const float F = B * a + E;
       float dNdF;
       const float Nv = ds(F, dNdF);
@@ -735,6 +759,171 @@ __global__ void affine_fit_kernel(const bf16* out, int ldo, int PH, int PW, int 
   }
 }
 
+// ---------------------------------------------------------------- full-image losses
+// compute_loss with edge / smooth terms (marigold_dc.py:195-235) needs the whole dense map, not only the
+// sparse pixels.  Three launches per guided step (only when loss_funcs is not {l1, l2}):
+//   dense_map    N (the clamped, learned-affine depth in the loss's depth space) at every (y, x)
+//   dense_grad   per pixel: dL/dN from the l1 / l2 term (sparse pixels, guide map) and from the four
+//                neighbour pairs of the edge / smooth terms (gathered, no atomics), chained through the
+//                depth space, clamp and affine into dA (resize adjoint) and per-block sums of the loss,
+//                dL/d(s^2 (max-min)) and dL/d(sh^2 min) in a fixed order
+//   dense_fold   one block per frame folds the block sums in order -> loss, d scale, d shift
+// flags: 1 l1, 2 l2, 4 edge, 8 smooth.  gray = 0.299 R + 0.587 G + 0.114 B of the uint8 image, in fp32
+// as torch forms it (uint8 * python float -> float32).
+struct DenseCtx {
+  const bf16* out;
+  int ldo, PH, PW, RH, RW, H, W;
+  const float* params;
+  const float* affine;
+};
+
+__device__ __forceinline__ float dense_value(const DenseCtx& c, int n, int y, int x, float& aff, float& F, float& dNdG,
+                                             Taps& t) {
+  const float* pr = c.params + n * 8;
+  aff = sample_affine(c.out, c.ldo, n, c.PH, c.PW, c.RH, c.RW, c.H, c.W, y, x, t, interp_nearest(pr));
+  const float s = c.affine[n * 2], sh = c.affine[n * 2 + 1];
+  const float B = (s * s) * (pr[5] - pr[4]);
+  F = B * aff + (sh * sh) * pr[4];
+  const DSpace ds(pr);
+  return ds(fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
+}
+
+__device__ __forceinline__ float gray_at(const unsigned char* img, int n, long HW, long p) {
+  const unsigned char* b = img + (long)n * 3 * HW + p;
+  return (0.299f * (float)b[0] + 0.587f * (float)b[HW]) + 0.114f * (float)b[2 * HW];
+}
+
+__device__ __forceinline__ float sgnf(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
+
+__global__ void dense_map_kernel(DenseCtx c, float* nmap) {
+  const int n = blockIdx.y;
+  const long HW = (long)c.H * c.W;
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+  float aff, F, dNdG;
+  Taps t;
+  nmap[n * HW + p] = dense_value(c, n, (int)(p / c.W), (int)(p % c.W), aff, F, dNdG, t);
+}
+
+// part[n][block][3] = (loss, sum dF * aff, sum dF)
+__global__ void dense_grad_kernel(DenseCtx c, const unsigned char* img, const float* nmap, const float* gmap,
+                                  const int* cnt, int flags, float* dA, float* part) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.y;
+  const int H = c.H, W = c.W;
+  const long HW = (long)H * W;
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float lsum = 0.0f, sdb = 0.0f, sde = 0.0f;
+  if (p < HW) {
+    const int y = (int)(p / W), x = (int)(p % W);
+    float aff, F, dNdG;
+    Taps t;
+    const float Nv = dense_value(c, n, y, x, aff, F, dNdG, t);
+    const float* nm = nmap + n * HW;
+    float gN = 0.0f;
+    // l1 / l2 at the sparse pixels (guide map holds NaN elsewhere)
+    const float gv = gmap[n * HW + p];
+    if ((flags & 3) && !__builtin_isnan(gv)) {
+      const float inv_cnt = 1.0f / (float)cnt[n];
+      const float r = Nv - gv;
+      if (flags & 1) { lsum += fabsf(r) * inv_cnt; gN += sgnf(r) * inv_cnt; }
+      if (flags & 2) { lsum += (r * r) * inv_cnt; gN += 2.0f * r * inv_cnt; }
+    }
+    if (flags & 12) {
+      const float icx = 1.0f / (float)((long)H * (W - 1)), icy = 1.0f / (float)((long)(H - 1) * W);
+      const bool edge = flags & 4, smooth = flags & 8;
+      float gp = 0.0f;
+      if (edge) gp = gray_at(img, n, HW, p);
+      // pair (p, right): owned by p (loss), contributes +c to p; pair (left, p): -c to p
+      auto pair = [&](float a, float b, float ga, float gb, float ic, bool own) {
+        const float d = a - b;
+        float cval = 0.0f;
+        if (edge) {
+          const float g = fabsf(ga - gb);
+          const float e = fabsf(d) - g;
+          if (own) lsum += fabsf(e) * ic;
+          cval += sgnf(e) * ic * sgnf(d);
+        }
+        if (smooth) {
+          if (own) lsum += fabsf(d) * ic;
+          cval += ic * sgnf(d);
+        }
+        return cval;
+      };
+      if (x + 1 < W) gN += pair(Nv, nm[p + 1], gp, edge ? gray_at(img, n, HW, p + 1) : 0.0f, icx, true);
+      if (x > 0) gN -= pair(nm[p - 1], Nv, edge ? gray_at(img, n, HW, p - 1) : 0.0f, gp, icx, false);
+      if (y + 1 < H) gN += pair(Nv, nm[p + W], gp, edge ? gray_at(img, n, HW, p + W) : 0.0f, icy, true);
+      if (y > 0) gN -= pair(nm[p - W], Nv, edge ? gray_at(img, n, HW, p - W) : 0.0f, gp, icy, false);
+    }
+    const float dF = (F >= 0.0f && F <= 1.0f) ? gN * dNdG : 0.0f;
+    sdb = dF * aff;
+    sde = dF;
+    if (dF != 0.0f) {
+      const float* pr = c.params + n * 8;
+      const float s = c.affine[n * 2];
+      const float B = (s * s) * (pr[5] - pr[4]);
+      const float dff = (float)(bf16)(dF * B);
+      float* dAn = dA + (long)n * c.PH * c.PW;
+      if (t.ly1 == 0.0f && t.lx1 == 0.0f && t.y0 == t.y1 && t.x0 == t.x1) {
+        atomicAdd(&dAn[(long)t.y0 * c.PW + t.x0], dff);
+      } else {
+        atomicAdd(&dAn[(long)t.y0 * c.PW + t.x0], t.ly0 * t.lx0 * dff);
+        atomicAdd(&dAn[(long)t.y0 * c.PW + t.x1], t.ly0 * t.lx1 * dff);
+        atomicAdd(&dAn[(long)t.y1 * c.PW + t.x0], t.ly1 * t.lx0 * dff);
+        atomicAdd(&dAn[(long)t.y1 * c.PW + t.x1], t.ly1 * t.lx1 * dff);
+      }
+    }
+  }
+  const float l = block_sum(lsum, scratch);
+  __syncthreads();
+  const float db = block_sum(sdb, scratch);
+  __syncthreads();
+  const float de = block_sum(sde, scratch);
+  if (threadIdx.x == 0) {
+    float* o = part + ((long)n * gridDim.x + blockIdx.x) * 3;
+    o[0] = l;
+    o[1] = db;
+    o[2] = de;
+  }
+}
+
+__global__ void dense_fold_kernel(const float* part, int nblk, const float* params, const float* affine,
+                                  float* daff_grad, float* loss) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.x;
+  float l = 0.0f, db = 0.0f, de = 0.0f;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+    const float* o = part + ((long)n * nblk + b) * 3;
+    l += o[0];
+    db += o[1];
+    de += o[2];
+  }
+  l = block_sum(l, scratch);
+  __syncthreads();
+  db = block_sum(db, scratch);
+  __syncthreads();
+  de = block_sum(de, scratch);
+  if (threadIdx.x == 0) {
+    const float* pr = params + n * 8;
+    const float s = affine[n * 2], sh = affine[n * 2 + 1];
+    daff_grad[n * 2] = (db * (pr[5] - pr[4])) * (2.0f * s);
+    daff_grad[n * 2 + 1] = (de * pr[4]) * (2.0f * sh);
+    loss[n] = l;
+  }
+}
+
+// dense guide map [nb][H*W]: the normalised guide at the sparse pixels, NaN elsewhere
+__global__ void guide_map_kernel(const int* idx, const float* gval, const int* cnt, long HW, float* gmap) {
+  const int n = blockIdx.y;
+  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += (long)gridDim.x * blockDim.x)
+    gmap[n * HW + p] = __int_as_float(0x7fc00000);
+}
+__global__ void guide_scatter_kernel(const int* idx, const float* gval, const int* cnt, long HW, float* gmap) {
+  const int n = blockIdx.y;
+  for (long k = (long)blockIdx.x * blockDim.x + threadIdx.x; k < cnt[n]; k += (long)gridDim.x * blockDim.x)
+    gmap[n * HW + idx[n * HW + k]] = gval[n * HW + k];
+}
+
 inline dim3 grid_for(long n) {
   long b = (n + 255) / 256;
   if (b > 65536) b = 65536;
@@ -744,13 +933,14 @@ inline dim3 grid_for(long n) {
 }  // namespace
 
 extern "C" int dc_sparse_setup(const float* sparse, int nb, int h, int w, int norm, float min_depth, float max_depth,
-                               const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt,
-                               float* params, void* stream) {
+                               const float* host_lohi, int projection, int inv, int interp, int* idx, float* gval,
+                               int* cnt, float* params, void* stream) {
   if (!sparse || !idx || !gval || !cnt || !params || nb <= 0 || h <= 0 || w <= 0) return DC_ERR_ARG;
-  if (norm < 0 || norm > 2 || projection < 0 || projection > 2) return DC_ERR_ARG;
+  if (norm < 0 || norm > 2 || projection < 0 || projection > 2 || inv < 0 || inv > 1 || interp < 0 || interp > 1)
+    return DC_ERR_ARG;
   if (norm == 2 && !host_lohi) return DC_ERR_ARG;
   hipLaunchKernelGGL(sparse_setup_kernel, dim3(nb), dim3(SETUP_THREADS), 0, (hipStream_t)stream, sparse, h, w, norm,
-                     min_depth, max_depth, host_lohi, projection, inv, idx, gval, cnt, params);
+                     min_depth, max_depth, host_lohi, projection, inv, interp, idx, gval, cnt, params);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -835,11 +1025,11 @@ extern "C" int dc_ddim_step(void* x8, const void* v, int nb, int hw, const float
 }
 
 extern "C" int dc_closed_form_affine(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h,
-                                     int w, const int* idx, const float* gval, const int* cnt, float* affine,
-                                     void* stream) {
-  if (!dec_out || !idx || !gval || !cnt || !affine || nb <= 0) return DC_ERR_ARG;
+                                     int w, const int* idx, const float* gval, const int* cnt, const float* params,
+                                     float* affine, void* stream) {
+  if (!dec_out || !idx || !gval || !cnt || !params || !affine || nb <= 0) return DC_ERR_ARG;
   hipLaunchKernelGGL(closed_form_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
-                     pw, rh, rw, h, w, idx, gval, cnt, affine);
+                     pw, rh, rw, h, w, idx, gval, cnt, params, affine);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -869,6 +1059,44 @@ extern "C" int dc_affine_fit(const void* dec_out, int ldo, int nb, int ph, int p
     return DC_ERR_ARG;
   hipLaunchKernelGGL(affine_fit_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
                      pw, rh, rw, h, w, idx, gval, cnt, params, train_steps, lr, opt, affine, loss);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" long long dc_dense_loss_ws_bytes(int nb, int h, int w) {
+  if (nb <= 0 || h <= 0 || w <= 0) return -1;
+  const long HW = (long)h * w;
+  const long nblk = (HW + 255) / 256;
+  return (long long)(nb * HW + nb * nblk * 3) * (long long)sizeof(float);
+}
+
+extern "C" int dc_guide_map(const int* idx, const float* gval, const int* cnt, int nb, int h, int w, float* gmap,
+                            void* stream) {
+  if (!idx || !gval || !cnt || !gmap || nb <= 0 || h <= 0 || w <= 0) return DC_ERR_ARG;
+  const long HW = (long)h * w;
+  const dim3 g((unsigned)min((HW + 255) / 256, 4096L), nb);
+  hipLaunchKernelGGL(guide_map_kernel, g, dim3(256), 0, (hipStream_t)stream, idx, gval, cnt, HW, gmap);
+  hipLaunchKernelGGL(guide_scatter_kernel, g, dim3(256), 0, (hipStream_t)stream, idx, gval, cnt, HW, gmap);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_dense_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                             const unsigned char* imgs, const float* gmap, const int* cnt, const float* params,
+                             const float* affine, int flags, float* ws, float* dA, float* daff_grad, float* loss,
+                             void* stream) {
+  if (!dec_out || !gmap || !cnt || !params || !affine || !ws || !dA || !daff_grad || !loss) return DC_ERR_ARG;
+  if (nb <= 0 || rh > ph || rw > pw || h < 2 || w < 2 || flags <= 0 || flags > 15) return DC_ERR_ARG;
+  if ((flags & 4) && !imgs) return DC_ERR_ARG;
+  const DenseCtx c{(const bf16*)dec_out, ldo, ph, pw, rh, rw, h, w, params, affine};
+  const long HW = (long)h * w;
+  const int nblk = (int)((HW + 255) / 256);
+  float* nmap = ws;
+  float* part = ws + (long)nb * HW;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(dense_map_kernel, dim3(nblk, nb), dim3(256), 0, st, c, nmap);
+  hipLaunchKernelGGL(dense_grad_kernel, dim3(nblk, nb), dim3(256), 0, st, c, imgs, nmap, gmap, cnt, flags, dA, part);
+  hipLaunchKernelGGL(dense_fold_kernel, dim3(nb), dim3(256), 0, st, part, nblk, params, affine, daff_grad, loss);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

@@ -30,6 +30,8 @@ from .unet import UNetHIP
 EPSILON = 1e-7                                   # marigold_dc.py:20
 SUPPORTED_LOSS_FUNCS = ["l1", "l2", "edge", "smooth"]   # marigold_dc.py:19
 _NORM = {"const": 0, "minmax": 1, "percentile": 2}
+_INTERP = {"bilinear": 0, "nearest": 1}
+_LOSS_BIT = {"l1": 1, "l2": 2, "edge": 4, "smooth": 8}
 _PROJ = {"linear": 0, "log": 1, "log10": 2}
 
 
@@ -187,14 +189,18 @@ class MarigoldDepthCompletionPipeline:
         opt_code = {"adam": 0, "sgd": 1, "adagrad": 2}[opt]
         # (per-input: the KL term reaches only the latents, which do not move)
         kld_code = {"simple": 1, "strict": 2}[kld_mode] if (kld and guided) else 0
-        unsupported = []
-        if optimised and sorted(loss_funcs) != ["l1", "l2"]:
-            unsupported.append(f"loss_funcs={loss_funcs}")
-        if interp_mode != "bilinear":
-            unsupported.append(f"interp_mode={interp_mode}")
-        if unsupported:
-            raise NotImplementedError("HIP path supports the l1 + l2 loss for the optimised modes; got "
-                                      + ", ".join(unsupported))
+        if interp_mode not in _INTERP:
+            raise ValueError(f"Unknown interp_mode: {interp_mode}")
+        # compute_loss terms (marigold_dc.py:131-245); {l1, l2} runs on the sparse pixels only
+        # (dc_sparse_loss), any other set on the whole dense map (dc_dense_loss)
+        loss_flags = 0
+        for f in loss_funcs:
+            loss_flags |= _LOSS_BIT[f]
+        full_loss = loss_flags != 3
+        if full_loss and (fit_affine or (guided and closed_form)):
+            raise NotImplementedError("HIP path: loss_funcs other than l1 + l2 are supported for the guided "
+                                      f"learned-affine mode only; got loss_funcs={loss_funcs} with "
+                                      f"{'closed_form' if guided else 'train_method=per-input'}")
         dev = self.device
         ctx = self.ctx
         imgs = imgs.to(dev)
@@ -240,12 +246,21 @@ class MarigoldDepthCompletionPipeline:
             sp_cpu = sparses.cpu()
             lohi = torch.stack([torch.quantile(s[s > 0], q) for s in sp_cpu]).to(dev).contiguous()
         _lib.call("dc_sparse_setup", sparses.data_ptr(), n, H, W, _NORM[norm], float(min_depth), float(max_depth),
-                  ops.P(lohi), _PROJ[projection], int(inv), idx.data_ptr(), gval.data_ptr(), cnt.data_ptr(),
-                  params.data_ptr(), ctx.stream)
+                  ops.P(lohi), _PROJ[projection], int(inv), _INTERP[interp_mode], idx.data_ptr(), gval.data_ptr(),
+                  cnt.data_ptr(), params.data_ptr(), ctx.stream)
         cnt_host = cnt.cpu()
         if (cnt_host == 0).any():
             raise ValueError("No valid values found in mask for some positions. "
                              "Ensure that mask has at least one True value along the specified dimensions.")
+        # full-image losses: dense guide map + the caller's uint8 image (edge term's gray gradients)
+        gmap = torch.empty(n, HWs, dtype=torch.float32, device=dev)
+        img_u8 = imgs.contiguous()
+        if full_loss and guided:
+            _lib.call("dc_guide_map", idx.data_ptr(), gval.data_ptr(), cnt.data_ptr(), n, H, W, gmap.data_ptr(),
+                      ctx.stream)
+            nws = _lib.load().dc_dense_loss_ws_bytes(n, H, W)
+            if st.get("dense_ws") is None or st["dense_ws"].numel() * 4 < nws:
+                st["dense_ws"] = torch.empty(-(-nws // 4), dtype=torch.float32, device=dev)
 
         # ---- per-call tables
         ts = self.scheduler.timesteps(steps)
@@ -258,16 +273,17 @@ class MarigoldDepthCompletionPipeline:
         st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))
         ops.memset(ctx, ctx.step)
         cf = bool(closed_form)
-        self._call_state = dict(idx=idx, gval=gval, cnt=cnt, params=params, coef=coef, adam=adam, H=H, W=W, RH=RH,
-                                RW=RW, PH=PH, PW=PW, n=n, h=h, w=w, cf=cf, opt=opt_code, kld=kld_code,
-                                kld_weight=float(kld_weight))
+        self._call_state = dict(idx=idx, gval=gval, cnt=cnt, params=params, coef=coef, adam=adam, gmap=gmap,
+                                img=img_u8, H=H, W=W, RH=RH, RW=RW, PH=PH, PW=PW, n=n, h=h, w=w, cf=cf,
+                                opt=opt_code, kld=kld_code, kld_weight=float(kld_weight),
+                                loss_flags=loss_flags if full_loss else 0)
 
         # ---- denoising loop (marigold_dc.py:800-909): guided steps, or plain DDIM steps
         step_fn = self._step if guided else self._ddim_step
         if self.use_graph:
             g = st["graph"]
             gkey = (guided, guided and cf, opt_code, kld_code, float(kld_weight), steps, H, W, RH, RW, lr_latent,
-                    lr_scaling)
+                    lr_scaling, loss_flags if full_loss else 0)
             if g is None or st["graph_key"] != gkey:
                 # tables are rebuilt per call at new addresses: capture against this call's buffers
                 g = torch.cuda.CUDAGraph()
@@ -283,11 +299,11 @@ class MarigoldDepthCompletionPipeline:
                 with torch.cuda.graph(g):
                     step_fn(st)
                 st["graph"], st["graph_key"] = g, gkey
-                st["graph_tables"] = (coef, adam, idx, gval, cnt, params)
+                st["graph_tables"] = (coef, adam, idx, gval, cnt, params, gmap, img_u8)
             else:
                 # replay reads the captured table addresses: refresh their contents in place
                 old = st["graph_tables"]
-                for dst, src in zip(old, (coef, adam, idx, gval, cnt, params)):
+                for dst, src in zip(old, (coef, adam, idx, gval, cnt, params, gmap, img_u8)):
                     dst.copy_(src)
             for _ in range(steps):
                 g.replay()
@@ -306,7 +322,8 @@ class MarigoldDepthCompletionPipeline:
                       float(lr_scaling), opt_code, st["affine"].data_ptr(), st["loss"].data_ptr(), ctx.stream)
         if closed_form:   # compute_affine_params on the final decode (marigold_dc.py:332-336)
             _lib.call("dc_closed_form_affine", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["idx"].data_ptr(),
-                      cs["gval"].data_ptr(), cs["cnt"].data_ptr(), st["affine"].data_ptr(), ctx.stream)
+                      cs["gval"].data_ptr(), cs["cnt"].data_ptr(), cs["params"].data_ptr(), st["affine"].data_ptr(),
+                      ctx.stream)
         _lib.call("dc_final_dense", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["params"].data_ptr(),
                   st["affine"].data_ptr(), int(bool(closed_form)), dense.data_ptr(), ctx.stream)
         lat = torch.empty(n, 4, h, w, dtype=BF16, device=dev)
@@ -317,8 +334,8 @@ class MarigoldDepthCompletionPipeline:
     def _tables(self, st):
         cs = self._call_state
         if self.use_graph and st.get("graph_tables") is not None:
-            coef, adam, idx, gval, cnt, params = st["graph_tables"]
-            return dict(cs, coef=coef, adam=adam, idx=idx, gval=gval, cnt=cnt, params=params)
+            coef, adam, idx, gval, cnt, params, gmap, img = st["graph_tables"]
+            return dict(cs, coef=coef, adam=adam, idx=idx, gval=gval, cnt=cnt, params=params, gmap=gmap, img=img)
         return cs
 
     def _reset_state(self, st, n, noise, prev, beta):
@@ -361,6 +378,11 @@ class MarigoldDepthCompletionPipeline:
             _lib.call("dc_sparse_loss_cf", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"],
                       cs["W"], cs["idx"].data_ptr(), cs["gval"].data_ptr(), cs["cnt"].data_ptr(),
                       cs["params"].data_ptr(), st["dA"].data_ptr(), st["loss"].data_ptr(), s)
+        elif cs["loss_flags"]:   # edge / smooth or a single point term: whole dense map
+            _lib.call("dc_dense_loss", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"],
+                      cs["W"], cs["img"].data_ptr(), cs["gmap"].data_ptr(), cs["cnt"].data_ptr(),
+                      cs["params"].data_ptr(), st["affine"].data_ptr(), cs["loss_flags"], st["dense_ws"].data_ptr(),
+                      st["dA"].data_ptr(), st["daff"].data_ptr(), st["loss"].data_ptr(), s)
         else:
             _lib.call("dc_sparse_loss", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"],
                       cs["W"], cs["idx"].data_ptr(), cs["gval"].data_ptr(), cs["cnt"].data_ptr(),

@@ -122,9 +122,11 @@ int dc_nchw_to_nhwc(const void* x, int nb, long long hw, int c, void* y, int ldy
  * params[nb][8] (dc_sparse_setup) = lo, hi, lo_p, hi_p, min_g, max_g, count, projection + 4 inv: the losses
  * compare in the projected / inverted depth space it names (marigold_dc.py:843-860).
  */
+/* interp: 0 bilinear, 1 nearest (the resize of _latent_to_affine, marigold_dc.py:366-370; stored in
+ * params[7] bit 3 for every kernel that samples the decoded map) */
 int dc_sparse_setup(const float* sparse, int nb, int h, int w, int norm, float min_depth, float max_depth,
-                    const float* host_lohi, int projection, int inv, int* idx, float* gval, int* cnt, float* params,
-                    void* stream);
+                    const float* host_lohi, int projection, int inv, int interp, int* idx, float* gval, int* cnt,
+                    float* params, void* stream);
 int dc_preview(const void* x8, const void* v, int nb, int hw, const float* coef, const int* step, void* x0, void* tin,
                float* eps_norm, void* stream);
 int dc_sparse_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w, const int* idx,
@@ -147,7 +149,8 @@ int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh,
 int dc_ddim_step(void* x8, const void* v, int nb, int hw, const float* coef, const int* step, void* stream);
 /* compute_affine_params (marigold_dc.py:53-128) over the sparse pixels: affine[nb][2] = scale, shift */
 int dc_closed_form_affine(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
-                          const int* idx, const float* gval, const int* cnt, float* affine, void* stream);
+                          const int* idx, const float* gval, const int* cnt, const float* params, float* affine,
+                          void* stream);
 /* guided steps with closed_form=True (marigold_dc.py:332-336 inside :828-877): loss of the closed-form fit
  * of the preview and its gradient dA, the fit (s, t) included in the differentiation */
 int dc_sparse_loss_cf(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
@@ -158,6 +161,16 @@ int dc_sparse_loss_cf(const void* dec_out, int ldo, int nb, int ph, int pw, int 
 int dc_affine_fit(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w, const int* idx,
                   const float* gval, const int* cnt, const float* params, int train_steps, float lr, int opt,
                   float* affine, float* loss, void* stream);
+/* compute_loss with the full-image terms (marigold_dc.py:131-245: l1, l2, edge, smooth; flags 1 | 2 | 4 | 8)
+ * on the learned-affine dense map of the guided step (replaces dc_sparse_loss when loss_funcs is not
+ * {l1, l2}): loss[nb], daff_grad[nb][2] and the resize-adjoint gradient added into dA [nb][ph][pw].
+ * imgs: the caller's uint8 [nb][3][h][w] (edge: gray = 0.299 R + 0.587 G + 0.114 B); gmap: dc_guide_map;
+ * ws: dc_dense_loss_ws_bytes(nb, h, w) bytes. */
+long long dc_dense_loss_ws_bytes(int nb, int h, int w);
+int dc_guide_map(const int* idx, const float* gval, const int* cnt, int nb, int h, int w, float* gmap, void* stream);
+int dc_dense_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                  const unsigned char* imgs, const float* gmap, const int* cnt, const float* params,
+                  const float* affine, int flags, float* ws, float* dA, float* daff_grad, float* loss, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
 
 #ifdef __cplusplus

@@ -235,3 +235,58 @@ def test_guided_optimisers_kld(kw):
 def test_per_input_optimisers(opt):
     _mode_parity(dict(norm="minmax", steps=5, train_method="per-input", train_steps=10, opt=opt, lr=(0.05, 0.05)),
                  26, f"per-input {opt}")
+
+
+@pytest.mark.parametrize("kw", [dict(loss_funcs=["l1", "l2", "edge", "smooth"]),
+                                dict(loss_funcs=["l1", "smooth"], norm="minmax"),
+                                dict(loss_funcs=["l2", "edge"], projection="log", min_depth=1.0),
+                                dict(loss_funcs=["l1"])])
+def test_guided_full_image_losses(kw):
+    """Guided steps with the edge / smooth terms of compute_loss (marigold_dc.py:195-235) or a single point
+    term: the loss runs on the whole dense map (dc_dense_loss)."""
+    _mode_parity(dict({"norm": "const"}, **kw, steps=6), 27, f"guided {kw}", fitted=True)
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(train_latents=False), dict(loss_funcs=["l1", "l2", "smooth"])])
+def test_nearest_interp(kw):
+    """interp_mode="nearest" for the resize of _latent_to_affine (marigold_dc.py:366-370): the decoded map is
+    upsampled 48x64 -> 50x70 here, so the nearest source index differs from bilinear's taps."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    n, h, w, res = 1, 50, 70, 64
+    cfg_o = tiny_unet_config()
+    imgs, sparses = synth_inputs(n, h, w, 60, seed=28)
+    eh, ew = -(-(res * h // max(h, w)) // 8), -(-(res * w // max(h, w)) // 8)
+    noise = torch.randn((1, 4, eh, ew), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
+    args = dict(kw, norm="const", steps=5, resolution=res, init_noise=noise, interp_mode="nearest")
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
+    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
+    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    torch.cuda.synchronize()
+    assert dh.shape == d32.shape and torch.isfinite(dh).all()
+    err_h, _ = fitted_error(dh, d32, sparses)
+    err_b, _ = fitted_error(d16, d32, sparses)
+    lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
+    lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
+    print(f"\nnearest {kw}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
+    assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
+    # blocky: every output pixel equals one decoded pixel, so the dense map has at most PH*PW levels per frame
+    assert dh.unique().numel() <= 48 * 64
+
+
+def test_full_loss_modes_not_silently_approximated():
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    cfg_o = tiny_unet_config()
+    unet = UNet2DConditionModel(cfg_o)
+    vae = AutoencoderTiny()
+    pipe = MarigoldDepthCompletionPipeline(synthetic_state_dict(unet, 1), synthetic_taesd_state_dict(vae, 2),
+                                           synthetic_text_embedding(3, 64), unet_config=TINY, device=dev)
+    imgs, sparses = synth_inputs(1, 48, 64, 60, seed=9)
+    with pytest.raises(NotImplementedError):
+        pipe(imgs, sparses, 120.0, resolution=64, steps=1, closed_form=True, loss_funcs=["l1", "edge"])
+    with pytest.raises(ValueError):
+        pipe(imgs, sparses, 120.0, resolution=64, steps=1, interp_mode="bicubic")
