@@ -77,7 +77,7 @@ def load_reference():
     """Return (namespace with the reference's functions, RefPipeline class)."""
     ns: dict = {"torch": torch, "Callable": Callable, "cast": cast, "nullcontext": nullcontext,
                 "SGD": SGD, "Adagrad": Adagrad, "Adam": Adam, "Optimizer": Optimizer}
-    ufuncs, _ = _extract(REF / "utils.py", {"kld_stdnorm", "masked_minmax"})
+    ufuncs, _ = _extract(REF / "utils.py", {"kld_stdnorm", "masked_minmax", "calc_bins", "mae", "rmse"})
     umod = ast.Module(body=ufuncs, type_ignores=[])
     uns: dict = {"torch": torch}
     exec(compile(umod, str(REF / "utils.py"), "exec"), uns)
@@ -195,6 +195,15 @@ def make_unit_vectors(ns, uns):
     for red in ("mean", "sum", "none"):
         for mode in ("simple", "strict"):
             out[f"kld_{mode}_{red}"] = uns["kld_stdnorm"](lat, reduction=red, mode=mode).reshape(-1)
+    # evaluation helpers of analyze.py (utils.py:162-192, 692-740)
+    for name, (lo, hi, size) in {"bins_default": (0.0, 120.0, 10.0), "bins_ragged": (2.5, 100.0, 7.5)}.items():
+        out[name] = torch.tensor(uns["calc_bins"](lo, hi, size), dtype=torch.float64)
+    dense = torch.rand((n, 1, h, w), generator=g) * 130.0
+    sparse = torch.where(mask, (guide * 40).round() * (120.0 / 255.0) * 5, torch.zeros(()))
+    out["eval_dense"], out["eval_sparse"] = dense, sparse
+    out["eval_mae"] = uns["mae"](dense, sparse, masks=mask).reshape(1)
+    out["eval_rmse"] = uns["rmse"](dense, sparse, masks=mask).reshape(1)
+    out["eval_mae_nomask"] = uns["mae"](dense, sparse).reshape(1)
     return {k: v.clone().contiguous() for k, v in out.items()}
 
 

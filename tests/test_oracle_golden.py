@@ -45,6 +45,13 @@ def test_unit_functions_match_reference():
     _same(mx, u["minmax_max"])
     for p in ("log", "log10", "linear"):
         _same(P.get_projection_fn(p)(guide), u["proj_" + p])
+    from oracle import analyze_ref as A
+    assert torch.equal(torch.tensor(A.calc_bins(0.0, 120.0, 10.0), dtype=torch.float64), u["bins_default"])
+    assert torch.equal(torch.tensor(A.calc_bins(2.5, 100.0, 7.5), dtype=torch.float64), u["bins_ragged"])
+    d, sp = u["eval_dense"], u["eval_sparse"]
+    _same(A.mae(d, sp, masks=mask).reshape(1), u["eval_mae"])
+    _same(A.rmse(d, sp, masks=mask).reshape(1), u["eval_rmse"])
+    _same(A.mae(d, sp).reshape(1), u["eval_mae_nomask"])
     for red in ("mean", "sum", "none"):
         for mode in ("simple", "strict"):
             _same(P.kld_stdnorm(lat, reduction=red, mode=mode).reshape(-1), u[f"kld_{mode}_{red}"])
