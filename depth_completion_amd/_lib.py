@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -32,7 +32,9 @@ class ConvDesc(C.Structure):
         ("bias", vp), ("rowbias", vp), ("rowbias_idx", vp), ("rowbias_ld", i32),
         ("resid", vp), ("ldr", i32), ("mask", vp), ("ldmask", i32), ("act", i32),
         ("y", vp), ("ldy", i32),
-        ("ws", vp), ("ws_bytes", i64), ("algo", i32), ("splitk", i32),
+        ("ws", vp), ("ws_bytes", i64),
+        ("geglu", i32), ("y2", vp), ("ldy2", i32), ("aux", vp), ("ldaux", i32),
+        ("algo", i32), ("splitk", i32),
     ]
 
 
@@ -76,8 +78,10 @@ _SIGS = {
     "dc_guide_map": [vp, vp, vp, i32, i32, i32, vp, vp],
     "dc_dense_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],
+    "dc_depth_metrics_ws_bytes": [],
+    "dc_depth_metrics": [vp, vp, i64, f32, f32, vp, i32, vp, vp, vp],
 }
-_RESTYPE = {"dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64}
+_RESTYPE = {"dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64}
 
 STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}
 

@@ -47,6 +47,11 @@ struct ConvGemmParams {
   int splits, kps;       // split-K: splits, k-chunks per split; stream-K: tile count, nk
   int* counters;        // [tiles] arrival counts, zero between launches (the workspace starts zeroed)
   int sk_blocks;        // > 0: stream-K over this many blocks (split-K / plain tiles: 0)
+  int geglu;            // GEGLU epilogue (include/dcamd.h): 0 none, 1 fwd (interleaved h/gate), 2 bwd
+  bf16* y2;
+  int ldy2;
+  const bf16* aux;
+  int ldaux;
 };
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of every padded / out-of-range piece
@@ -476,6 +481,50 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   constexpr int GPR = WN / 8;
+  if (p.geglu == 1) {
+    // (h, gate) column pairs 8 + 8: raw pre-activation to y, h * gelu(gate) to y2 (torch's bf16 rounding:
+    // gelu(gate) rounded, then the product)
+    constexpr int PPR = WN / 16;
+    for (int g = lane; g < WM * PPR; g += 64) {
+      const int row = g / PPR, pc = g - (g / PPR) * PPR;
+      const long m = m0 + wm * WM + row;
+      const int c = n0 + wn * WN + pc * 16;
+      if (m >= M || c >= p.cout) continue;
+      float h[8], gt[8], o[8];
+      load8(es + row * LDE + pc * 16, h);
+      load8(es + row * LDE + pc * 16 + 8, gt);
+      store8(p.y + m * p.ldy + c, h);
+      store8(p.y + m * p.ldy + c + 8, gt);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = h[k] * (float)(bf16)gelu_f(gt[k]);
+      store8(p.y2 + m * p.ldy2 + c / 2, o);
+    }
+    return;
+  }
+  if (p.geglu == 2) {
+    // dL/d(h * gelu(gate)) of 8 channels -> (dL/dh, dL/dgate) at their interleaved columns
+#pragma unroll 2
+    for (int g = lane; g < WM * GPR; g += 64) {
+      const int row = g / GPR, cg = g - (g / GPR) * GPR;
+      const long m = m0 + wm * WM + row;
+      const int c = n0 + wn * WN + cg * 8;
+      if (m >= M || c >= p.cout) continue;
+      float d[8], h[8], gt[8], dh[8], dg[8];
+      load8(es + row * LDE + cg * 8, d);
+      const long col = (long)(c / 8) * 16;
+      load8(p.aux + m * p.ldaux + col, h);
+      load8(p.aux + m * p.ldaux + col + 8, gt);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        dh[k] = d[k] * (float)(bf16)gelu_f(gt[k]);
+        const float dgel = (float)(bf16)(d[k] * h[k]);
+        dg[k] = dgel * gelu_grad(gt[k]);
+      }
+      store8(p.y + m * p.ldy + col, dh);
+      store8(p.y + m * p.ldy + col + 8, dg);
+    }
+    return;
+  }
 #pragma unroll 4
   for (int g = lane; g < WM * GPR; g += 64) {
     const int row = g / GPR, cg = g - (g / GPR) * GPR;
@@ -653,6 +702,15 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   p.ws = d->ws;
   p.ws_bytes = d->ws_bytes < (1L << 31) ? d->ws_bytes : (1L << 31);  // 32-bit buffer offsets
   p.splits = 1; p.kps = 0; p.counters = nullptr; p.sk_blocks = 0;
+  p.geglu = d->geglu;
+  p.y2 = (bf16*)d->y2; p.ldy2 = d->ldy2;
+  p.aux = (const bf16*)d->aux; p.ldaux = d->ldaux;
+  if (p.geglu < 0 || p.geglu > 2) return DC_ERR_ARG;
+  if (p.geglu) {  // plain linear / conv output only: no residual, mask, row bias or activation
+    if (p.resid || p.mask || p.rowbias || p.act || p.cout % 16) return DC_ERR_ARG;
+    if (p.geglu == 1 && (!p.y2 || p.ldy2 % 8 || ((uintptr_t)p.y2 & 15))) return DC_ERR_ARG;
+    if (p.geglu == 2 && (!p.aux || p.ldaux % 8 || ((uintptr_t)p.aux & 15) || p.ldy < 2 * p.cout)) return DC_ERR_ARG;
+  }
   // shape / alignment contract (host pads channels, see DESIGN.md "layouts")
   if (p.ktot % 64 != 0 || p.ktot < p.kh * p.kw * p.cin) return DC_ERR_ARG;
   if (p.cin % 8 != 0 || p.cout <= 0 || p.nb <= 0 || p.hout <= 0 || p.wout <= 0) return DC_ERR_ARG;

@@ -7,13 +7,6 @@
 
 namespace {
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
-
 // f: [rows][2c] = (h | g) ; y = h * gelu(g)
 __global__ void geglu_fwd_kernel(const bf16* f, int ldf, long rows, int c, bf16* y, int ldy) {
   const int cg = c / 8;

@@ -1,11 +1,10 @@
 // GroupNorm(+SiLU) and LayerNorm forward / backward on NHWC rows (gfx950).
 //
 // GroupNorm (diffusers ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out),
-// two launches, all reductions in a fixed order (bitwise reproducible run to run):
+// three launches, all reductions in a fixed order (bitwise reproducible run to run):
 //   stats     per (frame, pixel-chunk) block: 8 channels per thread in registers over its rows,
-//             rows folded through LDS, channels folded into group partials -> slab [nb][nchunk][G][2];
-//             the frame's last-arriving block folds the chunk partials (fp64) -> mean, rstd
-//             (a separate finalize launch only past kGnMaxFrames frames)
+//             rows folded through LDS, channels folded into group partials -> slab [nb][nchunk][G][2]
+//   finalize  one block per frame, one wave per group: fold the chunk partials (fp64) -> mean, rstd
 //   apply     elementwise normalise (+ SiLU), 16 B per lane
 // Backward: the same with (sum gamma*dy', sum gamma*dy'*xhat) and dx = rstd*(g*dy' - a - xhat*b).
 // The input may be two sources (UNet skip concat): channels >= c1 come from x2.
@@ -13,16 +12,6 @@
 #include "../../include/dcamd.h"
 
 namespace {
-
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-constexpr int kSc1 = 16;  // CPol::SC1 (device-coherent) on gfx950
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t gn_rsrc(const void* base) {
-  const unsigned long long a = (unsigned long long)base;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0, 0x7fffffff,
-                                           0x00020000);
-}
 
 struct GNShape {
   const bf16* x;
@@ -63,86 +52,15 @@ __device__ void gn_block_fold(const GNShape& s, const float* a, const float* b, 
     sb[ch] = tb;
   }
   __syncthreads();
-  const __amdgpu_buffer_rsrc_t r = gn_rsrc(out);
   for (int g = threadIdx.x; g < s.groups; g += blockDim.x) {
     float ta = 0.0f, tb = 0.0f;
     for (int k = 0; k < s.cpg; ++k) { ta += sa[g * s.cpg + k]; tb += sb[g * s.cpg + k]; }
-    // sc1: device-coherent hand-off to the frame's last-arriving block (gn_fold_frame)
-    __builtin_amdgcn_raw_buffer_store_b64(u32x2{__float_as_uint(ta), __float_as_uint(tb)}, r, g * 8, 0, kSc1);
+    out[g * 2] = ta;
+    out[g * 2 + 1] = tb;
   }
 }
 
-// Per-frame arrival counters of the stats passes (zero between launches: the last block resets its
-// frame's counter; kernel boundaries order the reset before the next launch).
-constexpr int kGnMaxFrames = 256;
-__device__ int g_gn_arrivals[kGnMaxFrames];
-
-// mean / rstd (mode 0) or the backward means (mode 1) of one (frame, group) from the folded sums
-__device__ __forceinline__ void gn_finish(double ta, double tb, double cnt, float eps, int mode, float* dst) {
-  if (mode == 0) {
-    const double mu = ta / cnt;
-    double var = tb / cnt - mu * mu;
-    if (var < 0.0) var = 0.0;
-    dst[0] = (float)mu;
-    dst[1] = (float)(1.0 / sqrt(var + (double)eps));
-  } else {
-    dst[0] = (float)(ta / cnt);
-    dst[1] = (float)(tb / cnt);
-  }
-}
-
-// Stats-pass tail: after its chunk partial is out, every block bumps its frame's counter; the block
-// that arrives last folds all chunk partials of the frame (fixed order: per group, thread `sub` sums
-// chunks sub, sub + nsub, ... in fp64, then the nsub sums in order) and writes out[n][G][2].  This
-// replaces a separate finalize launch (MI355X_MICROARCH.md hand-off table, row 1: sc1 stores, vmcnt(0),
-// barrier, one agent-scope add per block; the last adder reads with sc1 loads).
-__device__ void gn_stats_tail(const GNShape& s, int n, const float* part, float eps, int mode, float* out,
-                              float* sh) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int* flag = reinterpret_cast<int*>(sh);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(g_gn_arrivals + n, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = old == s.nchunk - 1;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  // thread t folds group pair gp = t % (G/2) over chunks cl, cl + ncl, ... (16-B sc1 loads of
-  // (a, b) for two groups, fp64 sums), then the ncl sums of each group are folded in order
-  const int G = s.groups, H = G >> 1, ncl = blockDim.x / H;
-  const int gp = threadIdx.x % H, cl = threadIdx.x / H;
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  if (cl < ncl) {
-    const __amdgpu_buffer_rsrc_t r = gn_rsrc(part + (long)n * s.nchunk * G * 2);
-    int k = cl;
-    for (; k + 7 * ncl < s.nchunk; k += 8 * ncl) {
-      f32x4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b128(r, ((k + j * ncl) * G + 2 * gp) * 8, 0, kSc1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { s0 += v[j][0]; s1 += v[j][1]; s2 += v[j][2]; s3 += v[j][3]; }
-    }
-    for (; k < s.nchunk; k += ncl) {
-      const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (k * G + 2 * gp) * 8, 0, kSc1);
-      s0 += v[0]; s1 += v[1]; s2 += v[2]; s3 += v[3];
-    }
-  }
-  double* dsh = reinterpret_cast<double*>(sh + 4);  // [ncl][G][2]
-  if (cl < ncl) {
-    double* d = dsh + ((long)cl * G + 2 * gp) * 2;
-    d[0] = s0; d[1] = s1; d[2] = s2; d[3] = s3;
-  }
-  __syncthreads();
-  if (threadIdx.x < G) {
-    const int g = threadIdx.x;
-    double fa = 0.0, fb = 0.0;
-    for (int j = 0; j < ncl; ++j) { fa += dsh[(j * G + g) * 2]; fb += dsh[(j * G + g) * 2 + 1]; }
-    gn_finish(fa, fb, (double)s.hw * s.cpg, eps, mode, out + ((long)n * G + g) * 2);
-  }
-  if (threadIdx.x == 0) g_gn_arrivals[n] = 0;
-}
-
-__global__ void gn_stats_kernel(GNShape s, float* part, float eps, float* stats) {
+__global__ void gn_stats_kernel(GNShape s, float* part) {
   extern __shared__ float sh[];
   const int n = blockIdx.y, chunk = blockIdx.x;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
@@ -157,7 +75,6 @@ __global__ void gn_stats_kernel(GNShape s, float* part, float eps, float* stats)
     }
   }
   gn_block_fold(s, a, b, sh, part + ((long)n * s.nchunk + chunk) * s.groups * 2);
-  if (stats) gn_stats_tail(s, n, part, eps, 0, stats, sh);
 }
 
 // one block per frame, one wave per group (looping): fp64 fold of the chunk partials.
@@ -190,7 +107,19 @@ __global__ void gn_finalize_kernel(GNShape s, const float* part, float eps, int 
       ta += __shfl_xor(ta, o, 64);
       tb += __shfl_xor(tb, o, 64);
     }
-    if (lane == 0) gn_finish(ta, tb, cnt, eps, mode, out + ((long)n * s.groups + g) * 2);
+    if (lane == 0) {
+      float* dst = out + ((long)n * s.groups + g) * 2;
+      if (mode == 0) {
+        const double mu = ta / cnt;
+        double var = tb / cnt - mu * mu;
+        if (var < 0.0) var = 0.0;
+        dst[0] = (float)mu;
+        dst[1] = (float)(1.0 / sqrt(var + (double)eps));
+      } else {
+        dst[0] = (float)(ta / cnt);
+        dst[1] = (float)(tb / cnt);
+      }
+    }
   }
 }
 
@@ -249,7 +178,7 @@ __device__ __forceinline__ void gn_bwd_elem(const GNShape& s, int n, int row, in
 }
 
 __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
-                                    const bf16* dy, int lddy, float* part, float* ab) {
+                                    const bf16* dy, int lddy, float* part) {
   extern __shared__ float sh[];
   const int n = blockIdx.y, chunk = blockIdx.x;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
@@ -264,7 +193,6 @@ __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* 
     }
   }
   gn_block_fold(s, a, b, sh, part + ((long)n * s.nchunk + chunk) * s.groups * 2);
-  if (ab) gn_stats_tail(s, n, part, 0.0f, 1, ab, sh);
 }
 
 __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
@@ -333,8 +261,8 @@ bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2,
   s.cpg = c / groups;
   s.cgs = c / 8;
   s.R = max(1, 256 / s.cgs);
-  // ~256 blocks over the whole launch, each at least R rows
-  const int target_blocks = max(1, 256 / nb);
+  // ~256-512 blocks over the whole launch, each at least R rows
+  const int target_blocks = max(1, 384 / nb);
   s.rows_per_chunk = max(s.R, (hw + target_blocks - 1) / target_blocks);
   s.rows_per_chunk = ((s.rows_per_chunk + s.R - 1) / s.R) * s.R;
   s.nchunk = (hw + s.rows_per_chunk - 1) / s.rows_per_chunk;
@@ -367,12 +295,8 @@ extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2
   hipStream_t st = (hipStream_t)stream;
   const int threads = s.cgs * s.R;
   const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
-  if (nb <= kGnMaxFrames && groups % 2 == 0) {  // stats + finalize in one launch (last block per frame folds)
-    hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws, eps, stats);
-  } else {
-    hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws, 0.0f, nullptr);
-    hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, eps, 0, stats);
-  }
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, eps, 0, stats);
   const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
   hipLaunchKernelGGL(gn_apply_kernel, agrid, dim3(threads), 0, st, s, stats, gamma, beta, silu, (bf16*)y, ldy);
   DC_CHECK_LAUNCH();
@@ -390,14 +314,9 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   const int threads = s.cgs * s.R;
   const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
   float* ab = ws + gn_part_floats(s);
-  if (nb <= kGnMaxFrames && groups % 2 == 0) {
-    hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, stats, gamma, beta, silu,
-                       (const bf16*)dy, lddy, ws, ab);
-  } else {
-    hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, stats, gamma, beta, silu,
-                       (const bf16*)dy, lddy, ws, nullptr);
-    hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
-  }
+  hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, stats, gamma, beta, silu,
+                     (const bf16*)dy, lddy, ws);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
   const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
   hipLaunchKernelGGL(gn_bwd_apply_kernel, agrid, dim3(threads), 0, st, s, stats, gamma, beta, silu,
                      (const bf16*)dy, lddy, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1, (const bf16*)add2,

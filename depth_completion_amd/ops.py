@@ -112,7 +112,8 @@ def conv_key(d) -> tuple:
 def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin: int, hout: int, wout: int,
               cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
               c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
-              y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None):
+              y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None, geglu: int = 0,
+              y2=None, aux=None):
     d = ConvDesc()
     d.x = P(x)
     d.ldx = LD(x)
@@ -135,6 +136,11 @@ def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     d.act = act
     d.y = P(y)
     d.ldy = LD(y)
+    d.geglu = geglu
+    d.y2 = P(y2)
+    d.ldy2 = LD(y2)
+    d.aux = P(aux)
+    d.ldaux = LD(aux)
     d.ws = ctx.ws.data_ptr() if splitk else None
     d.ws_bytes = ctx.ws_bytes if splitk else 0
     if algo is None:
@@ -194,10 +200,13 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3) -> tuple:
 
 
 def linear(ctx: Ctx, x, w: torch.Tensor, rows: int, cout: int, y, bias=None, resid=None, rowbias=None,
-           rowbias_ld: int = 0, act: int = 0):
-    """y[rows, cout] = x[rows, K] @ w[cout, K]^T (+ bias, + resid)."""
+           rowbias_ld: int = 0, act: int = 0, geglu: int = 0, y2=None, aux=None, algo: int | None = None,
+           nsplit: int | None = None):
+    """y[rows, cout] = x[rows, K] @ w[cout, K]^T (+ bias, + resid); geglu 1 / 2: the fused GEGLU
+    epilogues of include/dcamd.h (y2 = h * gelu(gate); aux = interleaved pre-activation)."""
     return conv_gemm(ctx, x, w, nb=1, hin=1, win=rows, cin=w.shape[1], hout=1, wout=rows, cout=cout, kh=1, kw=1,
-                     stride=1, pad=0, bias=bias, resid=resid, rowbias=rowbias, rowbias_ld=rowbias_ld, act=act, y=y)
+                     stride=1, pad=0, bias=bias, resid=resid, rowbias=rowbias, rowbias_ld=rowbias_ld, act=act, y=y,
+                     geglu=geglu, y2=y2, aux=aux, algo=algo, nsplit=nsplit)
 
 
 # ------------------------------------------------------------------------- norms

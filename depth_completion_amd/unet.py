@@ -16,7 +16,7 @@ import torch
 from . import ops
 from .config import UNetConfig
 from .ops import BF16, Ctx, Slice
-from .weights import Conv, Linear, Norm, fold_cross_attention, round_bf16
+from .weights import Conv, Linear, Norm, fold_cross_attention, geglu_interleave, round_bf16
 
 
 class ResnetW:
@@ -51,7 +51,9 @@ class TransformerW:
         self.out = Linear(sd[b + "attn1.to_out.0.weight"], sd[b + "attn1.to_out.0.bias"], dev)
         U, D, c0 = fold_cross_attention(sd, b + "attn2.", ctx, heads)
         self.U, self.D, self.c0 = U.to(dev), D.to(dev), c0.to(dev)
-        self.ff1 = Linear(sd[b + "ff.net.0.proj.weight"], sd[b + "ff.net.0.proj.bias"], dev)
+        # GEGLU projection with (h, gate) rows interleaved 8 + 8 for the fused epilogues (geglu_interleave)
+        perm = geglu_interleave(sd[b + "ff.net.0.proj.weight"].shape[0])
+        self.ff1 = Linear(sd[b + "ff.net.0.proj.weight"][perm], sd[b + "ff.net.0.proj.bias"][perm], dev)
         self.ff2 = Linear(sd[b + "ff.net.2.weight"], sd[b + "ff.net.2.bias"], dev)
         self.c = self.proj_in.cout
 
@@ -242,8 +244,7 @@ class UNetPlan:
             ops.linear(ctx, o, t.out.wf, P, C, r1, bias=t.out.bias, resid=p)
             ops.crossattn_fwd(ctx, r1, P, C, H, t.ln2.eps, t.ln2.gamma, t.ln2.beta, t.U, t.D, t.c0, r2, sl2, probs)
             ops.layernorm(ctx, r2, P, C, t.ln3.gamma, t.ln3.beta, t.ln3.eps, l3, sl3)
-            ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias)
-            ops.geglu(ctx, f8, P, 4 * C, gg)
+            ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias, geglu=1, y2=gg)   # + GEGLU
             ops.linear(ctx, gg, t.ff2.wf, P, C, r3, bias=t.ff2.bias, resid=r2)
             ops.linear(ctx, r3, t.proj_out.wf, P, C, out, bias=t.proj_out.bias, resid=x)
 
@@ -444,7 +445,6 @@ class UNetPlan:
         out = d["out"]
         dout = grad_of[id(out)]
         dr3 = self.buf(P, C)
-        dgg = self.buf(P, 4 * C)
         df = self.buf(P, 8 * C)
         dl3 = self.buf(P, C)
         dr2 = self.buf(P, C)
@@ -463,8 +463,7 @@ class UNetPlan:
 
         def b():
             ops.linear(ctx, dout, t.proj_out.wd, P, C, dr3)
-            ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, dgg)
-            ops.geglu_bwd(ctx, f8, P, 4 * C, dgg, df)
+            ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, df, geglu=2, aux=f8)   # + GEGLU backward
             ops.linear(ctx, df, t.ff1.wd, P, C, dl3)
             ops.layernorm_bwd(ctx, r2, P, C, t.ln3.gamma, sl3, dl3, dr2, add=dr3)
             ops.crossattn_bwd(ctx, r1, P, C, H, t.ln2.gamma, t.U, t.D, sl2, probs, dr2, dr1)

@@ -69,6 +69,15 @@ class Linear:
         self.wd = w.t().contiguous().to(device=device, dtype=BF16) if dgrad else None
 
 
+def geglu_interleave(n_out: int) -> torch.Tensor:
+    """Row order of the GEGLU projection (ff.net.0.proj, [2 * inner][C]) for the fused epilogue of
+    dc_conv_gemm (geglu = 1 / 2): blocks of 8 h rows then the 8 matching gate rows."""
+    inner = n_out // 2
+    blk = torch.arange(0, inner, 8)
+    idx = torch.stack([blk[:, None] + torch.arange(8), inner + blk[:, None] + torch.arange(8)], 1)
+    return idx.reshape(-1)
+
+
 class Norm:
     def __init__(self, w, b, device, eps):
         self.gamma = round_bf16(w).to(device)

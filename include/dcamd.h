@@ -52,6 +52,16 @@ typedef struct dc_conv_desc {
   int ldy;
   float* ws;       /* split-K workspace (may be NULL: no split-K) */
   long long ws_bytes;
+  /* GEGLU epilogues (diffusers GEGLU of the transformer FF, ff.net.0, fused into its two linears):
+   * 1: the output columns are (h, gate) pairs interleaved 8 + 8 (FF1 rows permuted at load); y gets the raw
+   *    pre-activation, y2[m][c/2 ..] = h * gelu(gate) (the [T][4C] input of FF2);
+   * 2: the output is dL/d(h * gelu(gate)) (FF2 input-gradient, 4C channels); with the pre-activation in aux
+   *    (interleaved layout) y gets (dL/dh, dL/dgate) interleaved 8 + 8 (the [T][8C] gradient of FF1's output) */
+  int geglu;
+  void* y2;
+  int ldy2;
+  const void* aux;
+  int ldaux;
   int algo;        /* 0 = heuristic, 1..dc_conv_num_algos(): tile/ring variant (plan-time autotuned) */
   int splitk;      /* 0 = heuristic, >=1 explicit K split, -1..-4 stream-K over 256..1024 blocks (needs ws) */
 } dc_conv_desc;
@@ -172,6 +182,15 @@ int dc_dense_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, 
                   const unsigned char* imgs, const float* gmap, const int* cnt, const float* params,
                   const float* affine, int flags, float* ws, float* dA, float* daff_grad, float* loss, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
+
+/* ---------------------------------------------------------------- evaluation (analyze.py)
+ * One batch of analyze.py:233-290 (utils.mae / utils.rmse, utils.py:692-740): mask = sparse > 0, both maps
+ * clamped to [min_depth, max_depth]; res[(1 + nbins)][3] = (sum |d - s|, sum (d - s)^2, count) overall and
+ * per bin (bins[nbins][2] = lo, hi, inclusive, on the clamped sparse depth; utils.calc_bins).  dense /
+ * sparse: fp32 device arrays of `total` elements; ws: dc_depth_metrics_ws_bytes() bytes. */
+long long dc_depth_metrics_ws_bytes(void);
+int dc_depth_metrics(const float* dense, const float* sparse, long long total, float min_depth, float max_depth,
+                     const float* bins, int nbins, double* ws, double* res, void* stream);
 
 #ifdef __cplusplus
 }

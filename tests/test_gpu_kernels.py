@@ -376,3 +376,38 @@ def test_conv_stream_k_unet_shape_deterministic(ctx, algo, nsplit):
         outs.append(y.clone())
     assert rel(nchw(outs[0], n, h, w), ref) < 1e-2
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("algo,nsplit", [(0, 0), (17, 1), (10, 3), (12, -1)])
+def test_geglu_epilogues(ctx, algo, nsplit):
+    """GEGLU fused into FF1's epilogue (geglu = 1: interleaved pre-activation + h * gelu(gate)) and into
+    FF2's input-gradient epilogue (geglu = 2: (dh, dgate) interleaved), vs torch fp32 on bf16 values."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import geglu_interleave
+    rows, c, inner = 300, 128, 256
+    x = rnd(rows, c, seed=60)
+    w1 = rnd(2 * inner, c, scale=1 / math.sqrt(c), seed=61)
+    b1 = rnd(2 * inner, seed=62)
+    perm = geglu_interleave(2 * inner)
+    f8 = torch.empty(rows, 2 * inner, dtype=torch.bfloat16, device=dev)
+    gg = torch.empty(rows, inner, dtype=torch.bfloat16, device=dev)
+    ops.linear(ctx, x.to(torch.bfloat16), w1[perm].to(torch.bfloat16).contiguous(), rows, 2 * inner, f8,
+               bias=b1[perm].contiguous(), geglu=1, y2=gg)
+    torch.cuda.synchronize()
+    pre = (x @ w1.t() + b1).to(torch.bfloat16).float()
+    h, g = pre[:, :inner], pre[:, inner:]
+    assert rel(f8.float(), pre[:, perm]) < 1e-2
+    assert rel(gg.float(), h * F.gelu(g).to(torch.bfloat16).float()) < 1e-2
+    # backward: dgg = dr @ W2 (W2 [c2][inner] as the FF2 weight, its dgrad weight is W2^T [inner][c2])
+    c2 = 192
+    dr = rnd(rows, c2, seed=63)
+    w2 = rnd(c2, inner, scale=1 / math.sqrt(inner), seed=64)
+    df = torch.empty(rows, 2 * inner, dtype=torch.bfloat16, device=dev)
+    ops.linear(ctx, dr.to(torch.bfloat16), w2.t().contiguous().to(torch.bfloat16), rows, inner, df, geglu=2,
+               aux=f8, algo=algo or None, nsplit=nsplit or None)
+    torch.cuda.synchronize()
+    dgg = (dr @ w2).to(torch.bfloat16).float()
+    hh, gq = h.clone().requires_grad_(), g.clone().requires_grad_()
+    (hh * F.gelu(gq)).backward(dgg)
+    ref = torch.cat([hh.grad, gq.grad], 1)[:, perm]
+    assert rel(df.float(), ref) < 1e-2
