@@ -6,9 +6,10 @@ Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across ra
 data-path collective (scaling = weak); the barrier + max-over-ranks timing is the only exchange.
 
 Also reported on the same JSON line:
-  roofline      the dominant kernel (implicit-GEMM conv/linear, dc_conv_gemm) timed with HIP events
-                on its launch stream around each launch of one live (eager) guided step:
-                algorithmic FLOPs / avg duration; `traffic` from the committed PMC pass
+  roofline      the dominant kernel (implicit-GEMM conv/linear, dc_conv_gemm): the time a graph-replayed
+                guided step spends in its conv launches (HIP events on the launch stream: the step's
+                graph minus the same graph without them), algorithmic FLOPs / avg duration; `traffic`
+                from the committed PMC pass
                 (profiles/pmc_conv_gemm.json, FETCH_SIZE x2 + WRITE_SIZE per launch, gfx950 correction)
   cpu_baseline  the oracle (CPU PyTorch restatement of the reference path, incl. weight-gradients as
                 the reference computes them) on this host's cores, rank 0 / N=1 only, on a bounded
@@ -56,41 +57,52 @@ def conv_flops(d) -> float:
     return f
 
 
-def measure_conv_kernel(pipe, st):
-    """Average duration of the dominant kernel (dc_conv_gemm) over one live guided step.
+def measure_conv_kernel(pipe, st, reps: int = 3):
+    """Time of the dominant kernel (dc_conv_gemm) inside one graph-replayed guided step.
 
-    One eager step of the pipeline runs with a pair of HIP events recorded on the launch stream
-    around every dc_conv_gemm launch, in the step's own order and cache state (no replays); the
-    events bracket each launch's GPU execution.  Returns (launches, summed duration ms, algorithmic
-    FLOPs) for the step.
+    The step is captured twice as a hipGraph: as the timed region runs it, and with every
+    dc_conv_gemm launch left out.  Each graph is replayed `reps` times between HIP events on the
+    launch stream; the difference is the time the step spends in its conv launches, in the step's
+    own order and cache state (no per-launch event packets).  Returns (launches, conv ms per step,
+    algorithmic FLOPs per step).
     """
     from depth_completion_amd import ops
     from depth_completion_amd._lib import ConvDesc
-    marks = []
+    descs = []
     orig = ops.call
 
-    def timed(name, *args):
-        if name != "dc_conv_gemm":
-            return orig(name, *args)
-        stream = torch.cuda.current_stream()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        r = orig(name, *args)
-        e1.record(stream)
-        marks.append((e0, e1, ConvDesc.from_buffer_copy(args[0]._obj)))
-        return r
+    def record(name, *args):
+        if name == "dc_conv_gemm":
+            descs.append(ConvDesc.from_buffer_copy(args[0]._obj))
+        return orig(name, *args)
 
-    ops.call = timed
-    try:
-        ops.memset(pipe.ctx, pipe.ctx.step)  # step index 0: per-step tables have exactly S rows
-        pipe._step(st)
-    finally:
-        ops.call = orig
+    def skip_conv(name, *args):
+        return None if name == "dc_conv_gemm" else orig(name, *args)
+
+    def timed_graph(hook):
+        g = torch.cuda.CUDAGraph()
+        ops.call = hook
+        try:
+            with torch.cuda.graph(g):
+                pipe._step(st)
+        finally:
+            ops.call = orig
+        stream = torch.cuda.current_stream()
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            g.replay()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+
     torch.cuda.synchronize()
-    total_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in marks)
-    flops = sum(conv_flops(d) for _, _, d in marks)
-    return len(marks), total_ms, flops
+    t_all = timed_graph(record)
+    n = len(descs)
+    t_rest = timed_graph(skip_conv)
+    flops = sum(conv_flops(d) for d in descs)
+    return n, max(t_all - t_rest, 1e-6), flops
 
 
 def cpu_baseline(h, w, n_points):
@@ -194,6 +206,7 @@ def main():
                 "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, C2 step)",
                 "kernel": "dc_conv_gemm = conv_gemm_kernel (split-K partials reduced in-kernel by the last block), implicit-GEMM conv/linear",
                 "launches_per_step": n_launch, "avg_launch_ms": round(avg_ms, 5),
+                "method": "graph-replayed step minus the same graph without its conv launches (HIP events)",
                 "algorithmic_gflop_per_step": round(conv_flops_ / 1e9, 1)}
     # whole-frame roofline: SURVEY §8(d) canonical 190.4 TFLOP per 768x576 frame (50 guided steps)
     frame_tflop = 190.4 * (args.denoise_steps / 50.0)

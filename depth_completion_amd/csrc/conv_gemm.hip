@@ -435,21 +435,29 @@ __device__ __forceinline__ bool tile_handoff(const ConvGemmParams& p, char* smem
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // (in row halves of the wave tile, to keep the register peak of the main loop's occupancy)
-  constexpr int MH = MI > 1 ? MI / 2 : 1;
+  // one accumulator row i at a time, GS segments' loads in flight per round (8 x 16 B per lane: the
+  // register peak stays that of the main loop's fragments), added in segment order -- one round trip
+  // per GS segments instead of per segment
+  constexpr int GS = NJ >= 8 ? 1 : 8 / NJ;
 #pragma unroll
-  for (int i0 = 0; i0 < MI; i0 += MH) {
-    for (int sp = 0; sp < narrive; ++sp) {
-      const long src = (long)slot_of(sp) * TILE_F + wid * (WM * WN) + lane * 4;
-      f32x4 part[MH][NJ];
+  for (int i = 0; i < MI; ++i) {
+    for (int sp0 = 0; sp0 < narrive; sp0 += GS) {
+      f32x4 part[GS][NJ];
 #pragma unroll
-      for (int i = 0; i < MH; ++i)
+      for (int g = 0; g < GS; ++g) {
+        if (sp0 + g < narrive) {
+          const long src = (long)slot_of(sp0 + g) * TILE_F + wid * (WM * WN) + lane * 4;
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) part[i][j] = load_sc1_x4(rs, src + ((i0 + i) * NJ + j) * 256);
+          for (int j = 0; j < NJ; ++j) part[g][j] = load_sc1_x4(rs, src + (i * NJ + j) * 256);
+        }
+      }
 #pragma unroll
-      for (int i = 0; i < MH; ++i)
+      for (int g = 0; g < GS; ++g) {
+        if (sp0 + g < narrive) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i0 + i][j] += part[i][j];
+          for (int j = 0; j < NJ; ++j) acc[i][j] += part[g][j];
+        }
+      }
     }
   }
   if (tid == 0) p.counters[tile] = 0;  // ready for the next launch (ordered by the kernel boundary)
