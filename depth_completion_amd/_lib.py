@@ -78,6 +78,11 @@ _SIGS = {
     "dc_guide_map": [vp, vp, vp, i32, i32, i32, vp, vp],
     "dc_dense_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],
+    "dc_latent_scale_fwd": [vp, i32, i64, f32, vp, vp],
+    "dc_latent_scale_bwd": [vp, i32, i64, f32, vp, vp, vp, vp, vp],
+    "dc_softmax_rows": [vp, i32, i64, i32, f32, vp, i32, vp],
+    "dc_softmax_rows_bwd": [vp, i32, vp, i32, i64, i32, f32, vp, i32, vp],
+    "dc_transpose": [vp, i32, i32, i32, vp, i32, vp],
     "dc_depth_metrics_ws_bytes": [],
     "dc_depth_metrics": [vp, vp, i64, f32, f32, vp, i32, vp, vp, vp],
 }

@@ -25,6 +25,7 @@ from . import _lib, ops
 from .config import MARIGOLD_V1, UNetConfig
 from .ops import BF16, Ctx
 from .taesd import TAESDHIP
+from .vae_kl import SD_VAE, AutoencoderKLHIP
 from .unet import UNetHIP
 
 EPSILON = 1e-7                                   # marigold_dc.py:20
@@ -77,7 +78,8 @@ class MarigoldDepthCompletionPipeline:
     """Guided-diffusion depth completion (Marigold-DC) on MI355X."""
 
     def __init__(self, unet_state: dict, vae_state: dict, text_embedding: torch.Tensor,
-                 unet_config: UNetConfig = MARIGOLD_V1, device="cuda", use_graph: bool = True):
+                 unet_config: UNetConfig = MARIGOLD_V1, device="cuda", use_graph: bool = True, vae: str = "light",
+                 vae_config=None):
         _lib.load()  # fail loudly without the HIP extension
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -85,7 +87,14 @@ class MarigoldDepthCompletionPipeline:
         self.dtype = BF16
         self.ctx = Ctx(self.device)
         self.unet = UNetHIP(unet_state, unet_config, self.device, text_embedding)
-        self.vae = TAESDHIP(vae_state, self.device)
+        # predict.py:44-52, 483-488: "light" = TAESD (AutoencoderTiny), "original" = the SD AutoencoderKL
+        if vae not in ("light", "original"):
+            raise ValueError(f"Unknown vae: {vae}")
+        self.vae_kind = vae
+        if vae == "light":
+            self.vae = TAESDHIP(vae_state, self.device)
+        else:
+            self.vae = AutoencoderKLHIP(vae_state, self.device, vae_config or SD_VAE)
         self.scheduler = DDIMTables()
         self.empty_text_embedding = text_embedding
         self.use_graph = use_graph
@@ -228,7 +237,9 @@ class MarigoldDepthCompletionPipeline:
 
         # ---- image latents (marigold_dc.py:687-698): preprocess + TAESD encoder into x8[..., 0:4]
         img8 = torch.empty(n * PH * PW, 8, dtype=BF16, device=dev)
-        _lib.call("dc_preprocess_image", imgs.contiguous().data_ptr(), n, H, W, RH, RW, PH, PW, 1, img8.data_ptr(),
+        # EncoderTiny maps [-1, 1] to [0, 1] itself; the KL encoder takes [-1, 1]
+        _lib.call("dc_preprocess_image", imgs.contiguous().data_ptr(), n, H, W, RH, RW, PH, PW,
+                  int(self.vae_kind == "light"), img8.data_ptr(),
                   ctx.stream)
         self.vae.encode(ctx, img8, n, PH, PW, ops.Slice(up.x8, 0))
         del img8
@@ -312,7 +323,7 @@ class MarigoldDepthCompletionPipeline:
                 step_fn(st)
 
         # ---- final decode (marigold_dc.py:969-985)
-        _lib.call("dc_taesd_clamp_fwd", ops.P(ops.Slice(up.x8, 4)), 8, P, dp.tin.data_ptr(), ctx.stream)
+        self._vae_input(ops.P(ops.Slice(up.x8, 4)), P, dp)
         dp.forward()
         dense = torch.empty(n, 1, H, W, dtype=torch.float32, device=dev)
         cs = self._tables(st)
@@ -330,6 +341,15 @@ class MarigoldDepthCompletionPipeline:
         _lib.call("dc_nhwc_to_nchw", ops.P(ops.Slice(up.x8, 4)), 8, n, h * w, 4, lat.data_ptr(), ctx.stream)
         self.last_loss = st["loss"]
         return dense, lat
+
+    def _vae_input(self, lat_ptr, P, dp):
+        """decode_prediction's VAE input from the latents at lat_ptr ([P][8] rows, 4 channels): TAESD's
+        tanh(x/3)*3 clamp, or z / scaling_factor for AutoencoderKL."""
+        if self.vae_kind == "light":
+            _lib.call("dc_taesd_clamp_fwd", lat_ptr, 8, P, dp.tin.data_ptr(), self.ctx.stream)
+        else:
+            _lib.call("dc_latent_scale_fwd", lat_ptr, 8, P, float(self.vae.cfg.scaling_factor), dp.tin.data_ptr(),
+                      self.ctx.stream)
 
     def _tables(self, st):
         cs = self._call_state
@@ -372,7 +392,10 @@ class MarigoldDepthCompletionPipeline:
         up.forward()                                                         # v = unet(cat(img, x_t), t)
         _lib.call("dc_preview", up.x8.data_ptr(), up.v.data_ptr(), n, h * w, cs["coef"].data_ptr(), step,
                   st["x0"].data_ptr(), dp.tin.data_ptr(), st["eps_norm"].data_ptr(), s)
-        dp.forward()                                                         # TAESD decode of x0
+        if self.vae_kind == "original":   # decode_prediction: vae.decode(x0 / scaling_factor)
+            _lib.call("dc_latent_scale_fwd", st["x0"].data_ptr(), 8, P, float(self.vae.cfg.scaling_factor),
+                      dp.tin.data_ptr(), s)
+        dp.forward()                                                         # VAE decode of x0
         ops.memset(ctx, st["dA"])
         if cs["cf"]:   # closed-form fit of the preview, differentiated (daff stays zero: no learned affine)
             _lib.call("dc_sparse_loss_cf", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"],
@@ -391,8 +414,12 @@ class MarigoldDepthCompletionPipeline:
         _lib.call("dc_decode_tail_bwd", dp.out.data_ptr(), 8, st["dA"].data_ptr(), n, cs["PH"], cs["PW"], cs["RH"],
                   cs["RW"], dp.dout.data_ptr(), s)
         dp.backward()                                                        # d tin
-        _lib.call("dc_taesd_clamp_bwd", st["x0"].data_ptr(), 8, dp.dtin.data_ptr(), 8, P, cs["coef"].data_ptr(), step,
-                  st["gdir"].data_ptr(), up.dv.data_ptr(), s)
+        if self.vae_kind == "light":   # backward of TAESD's tanh(x/3)*3, then of the Tweedie preview
+            _lib.call("dc_taesd_clamp_bwd", st["x0"].data_ptr(), 8, dp.dtin.data_ptr(), 8, P, cs["coef"].data_ptr(),
+                      step, st["gdir"].data_ptr(), up.dv.data_ptr(), s)
+        else:                          # backward of z / scaling_factor, then of the Tweedie preview
+            _lib.call("dc_latent_scale_bwd", dp.dtin.data_ptr(), 8, P, float(self.vae.cfg.scaling_factor),
+                      cs["coef"].data_ptr(), step, st["gdir"].data_ptr(), up.dv.data_ptr(), s)
         up.backward()                                                        # d x_t through the UNet
         _lib.call("dc_latent_update", up.x8.data_ptr(), up.v.data_ptr(), st["gdir"].data_ptr(), up.gx.data_ptr(), n,
                   h * w, cs["coef"].data_ptr(), cs["adam"].data_ptr(), step, st["eps_norm"].data_ptr(),

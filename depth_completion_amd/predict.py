@@ -8,8 +8,8 @@ Same arguments, defaults and coercions as the reference CLI (predict.py:25-457);
 * weights load from a local diffusers-format directory (``--weights DIR`` with ``unet/`` and
   ``taesd/`` safetensors plus ``empty_text_embedding.safetensors``) instead of the hub, or from
   seeded synthetic weights (``--synthetic-weights SEED``) -- there is no network;
-* ``--model lcm``, ``--vae original`` and ``--precision fp32`` are rows the HIP path does not run yet
-  and fail loudly; ``--compile-graph`` / ``--compile-mode`` are accepted and ignored (the step is
+* ``--model lcm`` and ``--precision fp32`` are rows the HIP path does not run yet and fail loudly
+  (``--vae original`` runs the AutoencoderKL of depth_completion_amd/vae_kl.py); ``--compile-graph`` / ``--compile-mode`` are accepted and ignored (the step is
   always a captured hipGraph);
 * under torch.distributed.run each rank processes a contiguous shard of every dataset's frames
   (depth_completion_amd/shard.py); ``--use-prev-latent`` chains stay inside a shard.
@@ -48,19 +48,25 @@ class CommaSeparated(click.ParamType):
             self.fail(f"{value!r} is not a comma-separated list of {self.typ.__name__}", param, ctx)
 
 
-def load_weights(weights: Path | None, synthetic_seed: int | None, unet_config: str):
+def load_weights(weights: Path | None, synthetic_seed: int | None, unet_config: str, vae: str = "light"):
+    """(unet state, VAE state, empty-prompt embedding, UNet config, VAE config): the light VAE is TAESD
+    (``taesd/``), the original one the Marigold checkpoint's AutoencoderKL (``vae/``)."""
     from . import synthetic
     from .config import MARIGOLD_V1, TINY
+    from .vae_kl import SD_VAE, TINY_KL
     cfg = TINY if unet_config == "tiny" else MARIGOLD_V1
+    kcfg = TINY_KL if unet_config == "tiny" else SD_VAE
     if weights is not None:
         from safetensors.torch import load_file
         unet = load_file(str(weights / "unet" / "diffusion_pytorch_model.safetensors"))
-        taesd = load_file(str(weights / "taesd" / "diffusion_pytorch_model.safetensors"))
+        sub = "taesd" if vae == "light" else "vae"
+        vsd = load_file(str(weights / sub / "diffusion_pytorch_model.safetensors"))
         emb = load_file(str(weights / "empty_text_embedding.safetensors"))["embedding"]
-        return unet, taesd, emb, cfg
+        return unet, vsd, emb, cfg, kcfg
     seed = 0 if synthetic_seed is None else synthetic_seed
-    return (synthetic.unet_state_dict(cfg, seed + 11), synthetic.taesd_state_dict(seed + 12),
-            synthetic.text_embedding(seed + 13, cfg.cross_attention_dim), cfg)
+    vsd = synthetic.taesd_state_dict(seed + 12) if vae == "light" else synthetic.kl_state_dict(kcfg, seed + 12)
+    return (synthetic.unet_state_dict(cfg, seed + 11), vsd, synthetic.text_embedding(seed + 13, cfg.cross_attention_dim),
+            cfg, kcfg)
 
 
 def discover(src_root: Path, use_segmask: bool):
@@ -211,8 +217,6 @@ def main(src_root, dst_root, model, vae, steps, res, norm, percentile, max_spars
     # ---- rows the HIP path does not run (fail loudly, never approximate)
     if model == "lcm":
         raise click.UsageError("--model lcm (LCMScheduler) is not implemented on the MI355X path")
-    if vae == "original":
-        raise click.UsageError("--vae original (AutoencoderKL) is a SURVEY §8f row not built yet")
     if precision == "fp32":
         raise click.UsageError("--precision fp32 is not supported: the MI355X kernels compute in bf16")
     if compile_graph:
@@ -230,8 +234,8 @@ def main(src_root, dst_root, model, vae, steps, res, norm, percentile, max_spars
     torch.cuda.set_device(dev)
 
     from .pipeline import MarigoldDepthCompletionPipeline
-    usd, vsd, emb, cfg = load_weights(weights, synthetic_weights, unet_config)
-    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=cfg, device=dev)
+    usd, vsd, emb, cfg, kcfg = load_weights(weights, synthetic_weights, unet_config, vae)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=cfg, device=dev, vae=vae, vae_config=kcfg)
     dst_root.mkdir(parents=True, exist_ok=True)
 
     for d, pairs, segmap in plan:

@@ -123,6 +123,58 @@ def _fan_in(shape):
     return shape[1] * (shape[2] * shape[3] if len(shape) == 4 else 1)
 
 
+def _kl_resnet(p, cin, cout):
+    s = [(p + "norm1.weight", (cin,), "norm"), (p + "norm1.bias", (cin,), "norm"),
+         (p + "conv1.weight", (cout, cin, 3, 3), "w"), (p + "conv1.bias", (cout,), ("b", cin * 9)),
+         (p + "norm2.weight", (cout,), "norm"), (p + "norm2.bias", (cout,), "norm"),
+         (p + "conv2.weight", (cout, cout, 3, 3), "w"), (p + "conv2.bias", (cout,), ("b", cout * 9))]
+    if cin != cout:
+        s += [(p + "conv_shortcut.weight", (cout, cin, 1, 1), "w"), (p + "conv_shortcut.bias", (cout,), ("b", cin))]
+    return s
+
+
+def _kl_mid(p, c):
+    s = _kl_resnet(p + "resnets.0.", c, c) + _kl_resnet(p + "resnets.1.", c, c)
+    a = p + "attentions.0."
+    s += [(a + "group_norm.weight", (c,), "norm"), (a + "group_norm.bias", (c,), "norm")]
+    for n in ("to_q", "to_k", "to_v", "to_out.0"):
+        s += [(a + n + ".weight", (c, c), "w"), (a + n + ".bias", (c,), ("b", c))]
+    return s
+
+
+def kl_shapes(cfg):
+    """AutoencoderKL (diffusers key layout) in the oracle module's registration order."""
+    ch, L, lc = cfg.block_out_channels, cfg.layers_per_block, cfg.latent_channels
+    s = [("encoder.conv_in.weight", (ch[0], 3, 3, 3), "w"), ("encoder.conv_in.bias", (ch[0],), ("b", 27))]
+    prev = ch[0]
+    for i, c in enumerate(ch):
+        for j in range(L):
+            s += _kl_resnet(f"encoder.down_blocks.{i}.resnets.{j}.", prev if j == 0 else c, c)
+        if i < len(ch) - 1:
+            p = f"encoder.down_blocks.{i}.downsamplers.0.conv."
+            s += [(p + "weight", (c, c, 3, 3), "w"), (p + "bias", (c,), ("b", c * 9))]
+        prev = c
+    s += _kl_mid("encoder.mid_block.", ch[-1])
+    s += [("encoder.conv_norm_out.weight", (ch[-1],), "norm"), ("encoder.conv_norm_out.bias", (ch[-1],), "norm"),
+          ("encoder.conv_out.weight", (2 * lc, ch[-1], 3, 3), "w"), ("encoder.conv_out.bias", (2 * lc,), ("b", ch[-1] * 9))]
+    rch = tuple(reversed(ch))
+    s += [("decoder.conv_in.weight", (rch[0], lc, 3, 3), "w"), ("decoder.conv_in.bias", (rch[0],), ("b", lc * 9))]
+    s += _kl_mid("decoder.mid_block.", rch[0])
+    prev = rch[0]
+    for i, c in enumerate(rch):
+        for j in range(L + 1):
+            s += _kl_resnet(f"decoder.up_blocks.{i}.resnets.{j}.", prev if j == 0 else c, c)
+        if i < len(rch) - 1:
+            p = f"decoder.up_blocks.{i}.upsamplers.0.conv."
+            s += [(p + "weight", (c, c, 3, 3), "w"), (p + "bias", (c,), ("b", c * 9))]
+        prev = c
+    s += [("decoder.conv_norm_out.weight", (rch[-1],), "norm"), ("decoder.conv_norm_out.bias", (rch[-1],), "norm"),
+          ("decoder.conv_out.weight", (3, rch[-1], 3, 3), "w"), ("decoder.conv_out.bias", (3,), ("b", rch[-1] * 9))]
+    s += [("quant_conv.weight", (2 * lc, 2 * lc, 1, 1), "w"), ("quant_conv.bias", (2 * lc,), ("b", 2 * lc)),
+          ("post_quant_conv.weight", (lc, lc, 1, 1), "w"), ("post_quant_conv.bias", (lc,), ("b", lc))]
+    return s
+
+
 def generate(shapes, seed: int, gain: float = 1.0, bias_bound: float | None = None) -> dict:
     g = torch.Generator().manual_seed(seed)
     sd = {}
@@ -152,3 +204,8 @@ def taesd_state_dict(seed: int = 12) -> dict:
 def text_embedding(seed: int = 13, cross_dim: int = 1024) -> torch.Tensor:
     g = torch.Generator().manual_seed(seed)
     return torch.randn((1, 2, cross_dim), generator=g)
+
+
+def kl_state_dict(cfg, seed: int = 12) -> dict:
+    """AutoencoderKL weights; equal to oracle.vae_kl_ref.synthetic_kl_state_dict for the same seed."""
+    return generate(kl_shapes(cfg), seed, gain=1.4)

@@ -183,6 +183,22 @@ int dc_dense_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, 
                   const float* affine, int flags, float* ws, float* dA, float* daff_grad, float* loss, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
 
+/* ---------------------------------------------------------------- AutoencoderKL (--vae original)
+ * decode_prediction's vae.decode(z / scaling_factor) (marigold_dc.py:366 via diffusers) for the 4 latent
+ * channels of a [P][ldx] bf16 row buffer -> y [P][8], and its backward chained into the Tweedie preview
+ * (as dc_taesd_clamp_bwd does for TAESD's tanh clamp).  The VAE mid-block attention (1 head of C = 512
+ * channels, diffusers Attention via SDPA) runs as dc_conv_gemm GEMMs around a row softmax:
+ * dc_softmax_rows: P = softmax(S * scale) per row (columns >= cols of P zeroed up to ldp);
+ * dc_softmax_rows_bwd: dS = P (dP - rowsum(P dP)) * scale; dc_transpose: y[c][r] = x[r][c], rows padded
+ * with zeros up to ldy. */
+int dc_latent_scale_fwd(const void* x, int ldx, long long pixels, float scale, void* y, void* stream);
+int dc_latent_scale_bwd(const void* dy, int lddy, long long pixels, float scale, const float* coef, const int* step,
+                        void* gx_direct, void* dv, void* stream);
+int dc_softmax_rows(const void* s, int lds, long long rows, int cols, float scale, void* p, int ldp, void* stream);
+int dc_softmax_rows_bwd(const void* p, int ldp, const void* dp, int lddp, long long rows, int cols, float scale,
+                        void* ds, int ldds, void* stream);
+int dc_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, void* stream);
+
 /* ---------------------------------------------------------------- evaluation (analyze.py)
  * One batch of analyze.py:233-290 (utils.mae / utils.rmse, utils.py:692-740): mask = sparse > 0, both maps
  * clamped to [min_depth, max_depth]; res[(1 + nbins)][3] = (sum |d - s|, sum (d - s)^2, count) overall and

@@ -147,8 +147,11 @@ class MarigoldBase:
         self.device = torch.device(device)
 
     def prepare_latents(self, image, latents, generator, ensemble_size, batch_size):
-        """[D] MarigoldDepthPipeline.prepare_latents (TAESD: ``.latents``, scaling_factor 1.0)."""
-        enc = [self.vae.encode(image[i:i + batch_size]).latents for i in range(0, image.shape[0], batch_size)]
+        """[D] MarigoldDepthPipeline.prepare_latents: retrieve_latents -> ``.latent_dist.mode()`` (AutoencoderKL)
+        or ``.latents`` (TAESD), times the VAE's scaling_factor (0.18215 / 1.0)."""
+        def retrieve(out):
+            return out.latent_dist.mode() if hasattr(out, "latent_dist") else out.latents
+        enc = [retrieve(self.vae.encode(image[i:i + batch_size])) for i in range(0, image.shape[0], batch_size)]
         img_lat = torch.cat(enc, dim=0) * self.vae.scaling_factor
         img_lat = img_lat.repeat_interleave(ensemble_size, dim=0)
         pred = latents

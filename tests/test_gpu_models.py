@@ -132,3 +132,58 @@ def test_taesd_decoder_encoder(ctx):
     e_enc = rel(from_nhwc(lat, n, h, w, 4), ref)
     print(f"taesd enc err {e_enc:.4f}")
     assert e_enc < 2e-2
+
+
+@pytest.mark.parametrize("which,n,h,w", [("tiny", 2, 6, 8), ("sd", 1, 4, 6)])
+def test_autoencoder_kl(ctx, which, n, h, w):
+    """AutoencoderKL (--vae original): decoder forward + input-gradient of vae.decode(z) and the encoder's
+    scaled posterior mean (prepare_latents), against the oracle's restatement of diffusers' modules
+    (oracle/vae_kl_ref.py), fp32 and bf16 executions; the SD config exercises the 512-channel single-head
+    mid attention."""
+    from oracle.vae_kl_ref import AutoencoderKL, KLConfig, synthetic_kl_state_dict
+    from depth_completion_amd.vae_kl import SD_VAE, TINY_KL, AutoencoderKLHIP
+    hcfg = TINY_KL if which == "tiny" else SD_VAE
+    ocfg = KLConfig(block_out_channels=hcfg.block_out_channels, layers_per_block=hcfg.layers_per_block)
+    vae = AutoencoderKL(ocfg)
+    sd = synthetic_kl_state_dict(vae, 21)
+    vae.load_state_dict(sd)
+    vae32 = vae.to(torch.bfloat16).float().to(dev)
+    vae16 = AutoencoderKL(ocfg)
+    vae16.load_state_dict(sd)
+    vae16 = vae16.to(torch.bfloat16).to(dev)
+    g = torch.Generator().manual_seed(4)
+    z = torch.randn(n, 4, h, w, generator=g).to(torch.bfloat16).float().to(dev)
+    zs = (z / 0.18215).to(torch.bfloat16).float().detach().requires_grad_(True)
+    out = vae32.decode(zs).sample
+    gout = torch.randn(out.shape, generator=torch.Generator().manual_seed(5)).to(torch.bfloat16).float().to(dev)
+    out.backward(gout)
+    zs16 = zs.detach().to(torch.bfloat16).requires_grad_(True)
+    out16 = vae16.decode(zs16).sample
+    out16.backward(gout.to(torch.bfloat16))
+    e_out16, e_g16 = rel(out16, out), rel(zs16.grad, zs.grad)
+    net = AutoencoderKLHIP({k: v.float() for k, v in sd.items()}, dev, hcfg)
+    dp = net.decoder_plan(ctx, n, h, w)
+    dp.tin.zero_()
+    dp.tin[:, :4].copy_(to_nhwc(zs.detach()).to(torch.bfloat16))
+    dp.forward()
+    dp.dout.zero_()
+    H, W = 8 * h, 8 * w
+    dp.dout[:, :3].copy_(to_nhwc(2 * gout).to(torch.bfloat16))   # out holds (decoder output + 1) / 2
+    dp.backward()
+    torch.cuda.synchronize()
+    e_out = rel(2 * from_nhwc(dp.out, n, H, W, 3) - 1, out)
+    e_g = rel(from_nhwc(dp.dtin, n, h, w, 4), zs.grad)
+    print(f"\nkl {which} dec out err {e_out:.4f} (oracle bf16 {e_out16:.4f}) grad err {e_g:.4f} (oracle bf16 {e_g16:.4f})")
+    assert e_out <= 2 * e_out16 + 2e-3 and e_g <= 2 * e_g16 + 2e-3
+    # encoder: mode() * scaling_factor of an image in [-1, 1]
+    img = (torch.rand(n, 3, H, W, generator=g) * 2 - 1).to(torch.bfloat16).float().to(dev)
+    ref = vae32.encode(img).latent_dist.mode() * 0.18215
+    ref16 = vae16.encode(img.to(torch.bfloat16)).latent_dist.mode() * 0.18215
+    x8 = torch.zeros(n * H * W, 8, dtype=torch.bfloat16, device=dev)
+    x8[:, :3].copy_(to_nhwc(img).to(torch.bfloat16))
+    lat = torch.zeros(n * h * w, 8, dtype=torch.bfloat16, device=dev)
+    net.encode(ctx, x8, n, H, W, lat)
+    torch.cuda.synchronize()
+    e_enc, e_enc16 = rel(from_nhwc(lat, n, h, w, 4), ref), rel(ref16, ref)
+    print(f"kl {which} enc err {e_enc:.4f} (oracle bf16 {e_enc16:.4f})")
+    assert e_enc <= 2 * e_enc16 + 2e-3

@@ -290,3 +290,47 @@ def test_full_loss_modes_not_silently_approximated():
         pipe(imgs, sparses, 120.0, resolution=64, steps=1, closed_form=True, loss_funcs=["l1", "edge"])
     with pytest.raises(ValueError):
         pipe(imgs, sparses, 120.0, resolution=64, steps=1, interp_mode="bicubic")
+
+
+@pytest.mark.parametrize("kw", [dict(), dict(train_latents=False)])
+def test_vae_original(kw):
+    """--vae original: the AutoencoderKL encoder (prepare_latents: latent_dist.mode() * 0.18215) and decoder
+    (decode_prediction: vae.decode(z / 0.18215)) in the guided loop / the plain DDIM mode, tiny configs."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    from depth_completion_amd.vae_kl import TINY_KL
+    from oracle.vae_kl_ref import AutoencoderKL, KLConfig, synthetic_kl_state_dict
+    n, h, w, res = 1, 48, 64, 64
+    cfg_o = tiny_unet_config()
+    imgs, sparses = synth_inputs(n, h, w, 60, seed=29)
+    noise = torch.randn((1, 4, 6, 8), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
+    args = dict(kw, norm="const", steps=5, resolution=res, init_noise=noise)
+    ocfg = KLConfig(block_out_channels=TINY_KL.block_out_channels, layers_per_block=TINY_KL.layers_per_block)
+    kl = AutoencoderKL(ocfg)
+    ksd = synthetic_kl_state_dict(kl, 31)
+    outs = {}
+    for dt in (torch.float32, torch.bfloat16):
+        unet = UNet2DConditionModel(cfg_o)
+        usd = synthetic_state_dict(unet, 11)
+        unet.load_state_dict(usd)
+        vae = AutoencoderKL(ocfg)
+        vae.load_state_dict(ksd)
+        emb = synthetic_text_embedding(13, cfg_o.cross_attention_dim)
+        o = P.OracleMarigoldDC(unet.to(dt).to(dev), vae.to(dt).to(dev), DDIMScheduler(), emb, dtype=dt, device=dev)
+        outs[dt] = o(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    pipe = MarigoldDepthCompletionPipeline(usd, ksd, emb, unet_config=TINY, device=dev, vae="original",
+                                           vae_config=TINY_KL)
+    dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    torch.cuda.synchronize()
+    (d32, l32), (d16, l16) = outs[torch.float32], outs[torch.bfloat16]
+    assert dh.shape == d32.shape and torch.isfinite(dh).all()
+    err_h, _ = fitted_error(dh, d32, sparses)
+    err_b, _ = fitted_error(d16, d32, sparses)
+    lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
+    lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
+    print(f"\nvae original {kw}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
+    # the VAE mid attention runs materialised (S, P, dP, dS stored in bf16; SDPA keeps them in fp32) and the
+    # guided loop's Adam steps amplify that extra rounding in the latents: 3x the bf16 oracle's own error
+    # there (measured 2.2x after 5 guided steps); the dense output keeps the 2x bound
+    k = 3 if kw.get("train_latents", True) else 2
+    assert err_h <= 2 * err_b + 2e-3 and lat_h <= k * lat_b + 2e-3

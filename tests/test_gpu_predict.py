@@ -9,7 +9,8 @@ from tests.test_predict_cli import make_dataset
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("extra", [[], ["--train-latents", "False"]])
+@pytest.mark.parametrize("extra", [[], ["--train-latents", "False"], ["--vae", "original"],
+                                   ["--loss-funcs", "l1,l2,edge", "--interp-mode", "nearest"]])
 def test_cli_end_to_end(tmp_path, extra):
     make_dataset(tmp_path / "data", n=2, h=48, w=64)
     out = tmp_path / "out"

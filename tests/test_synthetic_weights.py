@@ -28,3 +28,19 @@ def test_taesd_synthetic_matches_oracle():
     assert list(a.keys()) == list(b.keys())
     assert all(torch.equal(a[k], b[k]) for k in b)
     assert torch.equal(synthetic.text_embedding(13, 64), synthetic_text_embedding(13, 64))
+
+
+@pytest.mark.parametrize("which", ["tiny", "sd"])
+def test_kl_synthetic_matches_oracle(which):
+    from depth_completion_amd.vae_kl import SD_VAE, TINY_KL
+    from oracle.vae_kl_ref import AutoencoderKL, KLConfig, synthetic_kl_state_dict
+    hcfg = TINY_KL if which == "tiny" else SD_VAE
+    vae = AutoencoderKL(KLConfig(block_out_channels=hcfg.block_out_channels, layers_per_block=hcfg.layers_per_block))
+    shapes = synthetic.kl_shapes(hcfg)
+    ref = vae.state_dict()
+    assert [k for k, _, _ in shapes] == list(ref.keys())
+    assert all(tuple(ref[k].shape) == s for k, s, _ in shapes)
+    if which == "tiny":
+        a = synthetic.kl_state_dict(hcfg, 7)
+        b = synthetic_kl_state_dict(vae, 7)
+        assert all(torch.equal(a[k], b[k]) for k in b)
