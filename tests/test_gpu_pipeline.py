@@ -334,3 +334,41 @@ def test_vae_original(kw):
     # there (measured 2.2x after 5 guided steps); the dense output keeps the 2x bound
     k = 3 if kw.get("train_latents", True) else 2
     assert err_h <= 2 * err_b + 2e-3 and lat_h <= k * lat_b + 2e-3
+
+
+@pytest.mark.parametrize("h,w,npts,density", [(352, 1216, 0, 0.05), (900, 1600, 3000, 0.0)])
+def test_baseline_config_shapes(h, w, npts, density):
+    """BASELINE.json configs C4 (KITTI 1216x352: resized 222x768, padded to 224 -- latent 28x96 -- and
+    unpadded / resized back; 64-beam-like LiDAR rows) and C5 (nuScenes 1600x900: latent 54x96, 3000 points)
+    at processing resolution 768 through the tiny UNet, against the oracle."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    g = torch.Generator().manual_seed(30)
+    imgs, sparses = synth_inputs(1, h, w, npts, seed=30)
+    if density:   # 64 scan rows over the lower 60 % of the image, each pixel kept with p = 0.25 (SURVEY §8d)
+        rows = torch.linspace(0.4 * h, h - 1, 64).round().long()
+        keep = torch.zeros(h, w, dtype=torch.bool)
+        keep[rows] = torch.rand(64, w, generator=g) < 0.25
+        yy, xx = torch.meshgrid(torch.linspace(0, 1, h), torch.linspace(0, 1, w), indexing="ij")
+        field = ((10 + 80 * yy + 20 * xx) * 255 / 120).round().clamp(1, 255) * 120 / 255
+        sparses = torch.where(keep, field, torch.zeros(()))[None, None]
+    res = 768
+    eh, ew = -(-(res * h // max(h, w)) // 8), -(-(res * w // max(h, w)) // 8)
+    noise = torch.randn((1, 4, eh, ew), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
+    args = dict(norm="const", steps=3, resolution=res, init_noise=noise)
+    cfg_o = tiny_unet_config()
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
+    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
+    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    torch.cuda.synchronize()
+    assert dh.shape == (1, 1, h, w) and lh.shape == (1, 4, eh, ew) and torch.isfinite(dh).all()
+    err_h, p99_h = fitted_error(dh, d32, sparses)
+    err_b, p99_b = fitted_error(d16, d32, sparses)
+    lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
+    lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
+    print(f"\n{w}x{h}: HIP |d| {err_h:.5f} p99 {p99_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} "
+          f"latent {lat_b:.4f}")
+    assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
