@@ -47,6 +47,14 @@ def synth_frame(h, w, n_points, seed):
     return img, sp.view(1, h, w)
 
 
+def workload_name(h: int, w: int, batch: int) -> str:
+    """BASELINE.json configs: C2 / C3 (768x576, 1 / 8 frames), C4 (KITTI 1216x352), C5 (nuScenes 1600x900,
+    one seed of the ensemble); anything else is a custom shape."""
+    if (h, w) == (576, 768):
+        return "C2" if batch == 1 else "C3" if batch == 8 else f"C2-batch{batch}"
+    return {(352, 1216): "C4", (900, 1600): "C5 (single seed)"}.get((h, w), "custom")
+
+
 def conv_flops(d) -> float:
     """Algorithmic FLOPs of one dc_conv_gemm launch (real channels, valid taps only)."""
     M = d.nb * d.hout * d.wout
@@ -225,7 +233,7 @@ def main():
             "value": round(value, 4), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"workload": f"C{2 if B == 1 else 3}: {W}x{H} RGB + {args.points}-pt sparse depth, "
+            "config": {"workload": f"{workload_name(H, W, B)}: {W}x{H} RGB + {args.points}-pt sparse depth, "
                                    f"{args.denoise_steps} guided DDIM steps, {B} frame(s) per call per GPU",
                        "frames_per_step": B * world, "resolution": 768, "guided_steps": args.denoise_steps,
                        "parallelism": f"frame-sharded dp{world} (no collectives)",
