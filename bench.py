@@ -206,9 +206,11 @@ def main():
     achieved = conv_flops_ / (conv_ms * 1e-3) / 1e12
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_conv_gemm.json")
-    if B == 1 and os.path.exists(pmc):   # committed PMC pass of the C2 step (tools/pmc_traffic.py)
+    if os.path.exists(pmc):   # committed PMC pass (tools/pmc_traffic.py), reported only for its own shape
         with open(pmc) as f:
-            traffic = round(json.load(f)["traffic_bytes_per_launch"])
+            rec = json.load(f)
+        if rec.get("latent_shape") == [B, pipe._call_state["h"], pipe._call_state["w"]]:
+            traffic = round(rec["traffic_bytes_per_launch"])
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                 "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, C2 step)",
