@@ -7,9 +7,14 @@
 //   finalize  one block per frame, one wave per group: fold the chunk partials (fp64) -> mean, rstd
 //   apply     elementwise normalise (+ SiLU), 16 B per lane
 // Backward: the same with (sum gamma*dy', sum gamma*dy'*xhat) and dx = rstd*(g*dy' - a - xhat*b).
+// Small group slices (UNet levels 2-3) take a single launch instead: one block per (frame, group),
+// see gn_group_fwd_kernel.
 // The input may be two sources (UNet skip concat): channels >= c1 come from x2.
 #include "common.h"
 #include "../../include/dcamd.h"
+
+#include <initializer_list>
+#include <stdlib.h>
 
 namespace {
 
@@ -244,6 +249,222 @@ __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* 
   }
 }
 
+// ---- single-launch GroupNorm: one block per (frame, group), both passes inside the block.
+// The 3-launch form pays two kernel boundaries and a cross-block fold per GN (≈ 10-15 µs per forward at
+// every UNet level, whatever the size); a block that owns a whole group needs no hand-off at all.
+// Thread (v, r0) reads VEC channels (the v-th vector of the group's cpg channels) of rows r0, r0 + RP,
+// ..., U rows' loads in flight at once (one CU streams the whole group slice, so the pass is bound by
+// the bytes it keeps in flight); sums go to fp64 through a fixed-order block reduction (bitwise
+// reproducible).  Pass 1 stashes what it read in LDS (the slice is at most 138 KB per tensor at the
+// C2 shapes; the host only takes this path when it fits), and pass 2 reads it back from there: each
+// thread re-reads only its own slots, so no barrier guards the stash.  Blocks are dealt so that one XCD
+// owns a contiguous range of groups (its L2 holds its own channel slice of each row).
+template <int VEC>
+using bfvec = __bf16 __attribute__((ext_vector_type(VEC)));
+
+constexpr int kGroupThreads = 1024;
+constexpr int kGroupRed = 32 * sizeof(double);          // reduction scratch in front of the stash
+constexpr long kGroupLds = 160 * 1024;                   // LDS per workgroup on gfx950
+
+__device__ __forceinline__ int gn_group_block(int nblk) {
+  const int b = blockIdx.x;
+  return (nblk & 7) ? b : (b & 7) * (nblk >> 3) + (b >> 3);
+}
+
+__device__ __forceinline__ const bf16* gn_group_src(const GNShape& s, int n, int ch, long& ld) {
+  if (ch < s.c1) {
+    ld = s.ldx;
+    return s.x + (long)n * s.hw * s.ldx + ch;
+  }
+  ld = s.ldx2;
+  return s.x2 + (long)n * s.hw * s.ldx2 + (ch - s.c1);
+}
+
+// fixed-order fp64 block reduction of (a, b) over the block's waves; result in every thread
+__device__ __forceinline__ void gn_group_reduce(float a, float b, double* red, double& ta, double& tb) {
+  double da = a, db = b;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    da += __shfl_xor(da, o, 64);
+    db += __shfl_xor(db, o, 64);
+  }
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w] = da;
+    red[16 + w] = db;
+  }
+  __syncthreads();
+  ta = 0.0;
+  tb = 0.0;
+  for (int k = 0; k < nw; ++k) {
+    ta += red[k];
+    tb += red[16 + k];
+  }
+}
+
+template <int VEC, int U>
+__global__ __launch_bounds__(kGroupThreads) void gn_group_fwd_kernel(GNShape s, int vpr, int RP, float eps,
+                                                                    const float* gamma, const float* beta, int silu,
+                                                                    bf16* y, int ldy, float* stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* red = reinterpret_cast<double*>(smem);
+  bfvec<VEC>* stash = reinterpret_cast<bfvec<VEC>*>(smem + kGroupRed);
+  const int L = gn_group_block(s.nb * s.groups);
+  const int n = L / s.groups, g = L % s.groups;
+  const int v = threadIdx.x % vpr, r0 = threadIdx.x / vpr;
+  const bool act = r0 < RP;
+  const int ch = g * s.cpg + v * VEC;
+  long ld;
+  const bf16* src = gn_group_src(s, n, ch, ld);
+  float s1 = 0.0f, s2 = 0.0f;
+  if (act) {
+    for (int r = r0; r < s.hw; r += RP * U) {
+      bfvec<VEC> raw[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r + u * RP;
+        raw[u] = row < s.hw ? *reinterpret_cast<const bfvec<VEC>*>(src + row * ld) : bfvec<VEC>{};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r + u * RP;
+        if (row < s.hw) stash[row * vpr + v] = raw[u];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float f = (float)raw[u][i];
+          s1 += f;
+          s2 += f * f;
+        }
+      }
+    }
+  }
+  double ta, tb;
+  gn_group_reduce(s1, s2, red, ta, tb);
+  const double cnt = (double)s.hw * s.cpg;
+  const double mu_d = ta / cnt;
+  double var = tb / cnt - mu_d * mu_d;
+  if (var < 0.0) var = 0.0;
+  const float mu = (float)mu_d, rs = (float)(1.0 / sqrt(var + (double)eps));
+  if (threadIdx.x == 0) {
+    stats[((long)n * s.groups + g) * 2] = mu;
+    stats[((long)n * s.groups + g) * 2 + 1] = rs;
+  }
+  if (!act) return;
+  float ga[VEC], be[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    ga[i] = gamma[ch + i];
+    be[i] = beta[ch + i];
+  }
+  bf16* dst = y + (long)n * s.hw * ldy + ch;
+  for (int row = r0; row < s.hw; row += RP) {
+    const bfvec<VEC> raw = stash[row * vpr + v];
+    bfvec<VEC> o;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float t = ((float)raw[i] - mu) * rs * ga[i] + be[i];
+      if (silu) t = silu_f((float)(bf16)t);
+      o[i] = (bf16)t;
+    }
+    *reinterpret_cast<bfvec<VEC>*>(dst + (long)row * ldy) = o;
+  }
+}
+
+template <int VEC, int U>
+__global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, int vpr, int RP, const float* stats,
+                                                                    const float* gamma, const float* beta, int silu,
+                                                                    const bf16* dy, int lddy, bf16* dx, int lddx,
+                                                                    const bf16* add1, int ldadd1, const bf16* add2,
+                                                                    int ldadd2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* red = reinterpret_cast<double*>(smem);
+  bfvec<VEC>* sx = reinterpret_cast<bfvec<VEC>*>(smem + kGroupRed);
+  bfvec<VEC>* sd = sx + (long)s.hw * vpr;
+  const int L = gn_group_block(s.nb * s.groups);
+  const int n = L / s.groups, g = L % s.groups;
+  const int v = threadIdx.x % vpr, r0 = threadIdx.x / vpr;
+  const bool act = r0 < RP;
+  const int ch = g * s.cpg + v * VEC;
+  long ld;
+  const bf16* src = gn_group_src(s, n, ch, ld);
+  const bf16* dsrc = dy + (long)n * s.hw * lddy + ch;
+  const float mu = stats[((long)n * s.groups + g) * 2], rs = stats[((long)n * s.groups + g) * 2 + 1];
+  float ga[VEC], be[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    ga[i] = act ? gamma[ch + i] : 0.0f;
+    be[i] = act ? beta[ch + i] : 0.0f;
+  }
+  // dy' = dy * silu'(y) rounded as bf16 autograd does (gn_bwd_elem); returns g * dy' and xhat
+  auto elem = [&](float f, float d, int i, float& xh) {
+    xh = (f - mu) * rs;
+    float dd = d;
+    if (silu) {
+      const float yv = (float)(bf16)(xh * ga[i] + be[i]);
+      dd = (float)(bf16)(dd * silu_grad(yv));
+    }
+    return dd * ga[i];
+  };
+  float sa = 0.0f, sb = 0.0f;
+  if (act) {
+    for (int r = r0; r < s.hw; r += RP * U) {
+      bfvec<VEC> rx[U], rd[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r + u * RP;
+        const bool ok = row < s.hw;
+        rx[u] = ok ? *reinterpret_cast<const bfvec<VEC>*>(src + row * ld) : bfvec<VEC>{};
+        rd[u] = ok ? *reinterpret_cast<const bfvec<VEC>*>(dsrc + (long)row * lddy) : bfvec<VEC>{};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r + u * RP;
+        if (row >= s.hw) continue;
+        sx[row * vpr + v] = rx[u];
+        sd[row * vpr + v] = rd[u];
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          float xh;
+          const float gd = elem((float)rx[u][i], (float)rd[u][i], i, xh);
+          sa += gd;
+          sb += gd * xh;
+        }
+      }
+    }
+  }
+  double ta, tb;
+  gn_group_reduce(sa, sb, red, ta, tb);
+  const double cnt = (double)s.hw * s.cpg;
+  const float ma = (float)(ta / cnt), mb = (float)(tb / cnt);
+  if (!act) return;
+  bf16* dst = dx + (long)n * s.hw * lddx + ch;
+  const long pix0 = (long)n * s.hw;
+  for (int row = r0; row < s.hw; row += RP) {
+    const bfvec<VEC> rx = sx[row * vpr + v], rd = sd[row * vpr + v];
+    float out[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float xh;
+      const float gd = elem((float)rx[i], (float)rd[i], i, xh);
+      out[i] = rs * (gd - ma - xh * mb);
+    }
+    if (add1) {
+      const bfvec<VEC> e = *reinterpret_cast<const bfvec<VEC>*>(add1 + (pix0 + row) * ldadd1 + ch);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) out[i] = (float)(bf16)out[i] + (float)e[i];
+    }
+    if (add2) {
+      const bfvec<VEC> e = *reinterpret_cast<const bfvec<VEC>*>(add2 + (pix0 + row) * ldadd2 + ch);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) out[i] = (float)(bf16)out[i] + (float)e[i];
+    }
+    bfvec<VEC> o;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) o[i] = (bf16)out[i];
+    *reinterpret_cast<bfvec<VEC>*>(dst + (long)row * lddx) = o;
+  }
+}
+
 bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c,
                    int groups) {
   if (!x || nb <= 0 || hw <= 0 || c <= 0 || groups <= 0 || groups > 64) return false;
@@ -276,6 +497,41 @@ bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2,
 // workspace layout: [partials nb*nchunk*G*2][ab nb*G*2]
 inline long gn_part_floats(const GNShape& s) { return (long)s.nb * s.nchunk * s.groups * 2; }
 
+// Single-launch path selection: widest vector (8 / 4 / 2 channels) that divides the group and keeps
+// every operand aligned; 0 = take the 3-launch form.  Taken when the group slice of each stashed tensor
+// (hw * cpg * 2 bytes; the forward stashes x, the backward x and dy) is at most `cap` bytes: one CU
+// streams the slice with `cpg`-wide row segments (a fraction of each 128-B line), so the single launch
+// only wins where the slice is small -- measured (tools/gn_bench.py) up to ~70 KB forward, ~35 KB
+// backward at the UNet shapes.  DC_GN_GROUP=0 forces the 3-launch form, DC_GN_GROUP=<bytes> sets the
+// cap, DC_GN_GROUP=-1 lifts it to the LDS limit (A/B and tests).
+int gn_group_vec(const GNShape& s, int tensors, long cap, std::initializer_list<const void*> ptrs) {
+  if (const char* env = getenv("DC_GN_GROUP")) {   // read per call (host side only; graphs capture the choice)
+    const long v = atol(env);
+    if (v == 0) return 0;
+    cap = v < 0 ? kGroupLds : v;
+  }
+  const long slice = (long)s.hw * s.cpg * 2;
+  if (slice > cap || tensors * slice + kGroupRed > kGroupLds) return 0;
+  for (int vec = 8; vec >= 2; vec >>= 1) {
+    if (s.cpg % vec || s.cpg / vec > kGroupThreads) continue;
+    bool ok = true;
+    for (const void* p : ptrs) ok = ok && ((uintptr_t)p % (2 * vec) == 0);
+    if (ok) return vec;
+  }
+  return 0;
+}
+constexpr long kGroupCapFwd = 72 * 1024, kGroupCapBwd = 36 * 1024;
+
+// the stash may exceed the default 64 KB dynamic-LDS limit: raise it once per instantiation
+#define DC_GN_GROUP_LAUNCH(KERNEL, ...)                                                                      \
+  do {                                                                                                        \
+    static const hipError_t attr_ = hipFuncSetAttribute(reinterpret_cast<const void*>(&KERNEL),              \
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,           \
+                                                        (int)(kGroupLds - kGroupRed));                        \
+    (void)attr_;                                                                                              \
+    hipLaunchKernelGGL(KERNEL, grid, blk, lds, st, __VA_ARGS__);                                              \
+  } while (0)
+
 }  // namespace
 
 extern "C" long long dc_groupnorm_ws_bytes(int nb, int hw, int c, int groups) {
@@ -293,6 +549,20 @@ extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2
     return DC_ERR_ARG;
   if (ldy % 8) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
+  if (const int vec = gn_group_vec(s, 1, kGroupCapFwd, {s.x, s.x2, y})) {
+    const int vpr = s.cpg / vec, RP = kGroupThreads / vpr;
+    const dim3 grid(nb * groups), blk(kGroupThreads);
+    const size_t lds = kGroupRed + (size_t)hw * s.cpg * 2;
+    // U: 128 B of loads in flight per thread
+    if (vec == 8)
+      DC_GN_GROUP_LAUNCH((gn_group_fwd_kernel<8, 8>), s, vpr, RP, eps, gamma, beta, silu, (bf16*)y, ldy, stats);
+    else if (vec == 4)
+      DC_GN_GROUP_LAUNCH((gn_group_fwd_kernel<4, 16>), s, vpr, RP, eps, gamma, beta, silu, (bf16*)y, ldy, stats);
+    else
+      DC_GN_GROUP_LAUNCH((gn_group_fwd_kernel<2, 32>), s, vpr, RP, eps, gamma, beta, silu, (bf16*)y, ldy, stats);
+    DC_CHECK_LAUNCH();
+    return DC_OK;
+  }
   const int threads = s.cgs * s.R;
   const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
   hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws);
@@ -311,6 +581,23 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   if (!gn_make_shape(s, x, ldx, x2, ldx2, c1, nb, hw, c, groups) || !dy || !dx || !stats || !ws) return DC_ERR_ARG;
   if (lddy % 8 || lddx % 8 || (add1 && ldadd1 % 8) || (add2 && ldadd2 % 8)) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
+  if (const int vec = gn_group_vec(s, 2, kGroupCapBwd, {s.x, s.x2, dy, dx, add1 ? add1 : dx, add2 ? add2 : dx})) {
+    const int vpr = s.cpg / vec, RP = kGroupThreads / vpr;
+    const dim3 grid(nb * groups), blk(kGroupThreads);
+    const size_t lds = kGroupRed + 2 * (size_t)hw * s.cpg * 2;
+#define DC_GN_GROUP_BWD(V, U)                                                                                   \
+  DC_GN_GROUP_LAUNCH((gn_group_bwd_kernel<V, U>), s, vpr, RP, stats, gamma, beta, silu, (const bf16*)dy, lddy,  \
+                     (bf16*)dx, lddx, (const bf16*)add1, ldadd1, (const bf16*)add2, ldadd2)
+    if (vec == 8)
+      DC_GN_GROUP_BWD(8, 4);
+    else if (vec == 4)
+      DC_GN_GROUP_BWD(4, 8);
+    else
+      DC_GN_GROUP_BWD(2, 16);
+#undef DC_GN_GROUP_BWD
+    DC_CHECK_LAUNCH();
+    return DC_OK;
+  }
   const int threads = s.cgs * s.R;
   const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
   float* ab = ws + gn_part_floats(s);

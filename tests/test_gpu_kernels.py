@@ -145,8 +145,18 @@ def test_small_cin_and_splitk_linear(ctx):
 
 
 # ----------------------------------------------------------------------------- norms
-@pytest.mark.parametrize("c,silu,two", [(320, True, False), (640, False, False), (960, True, True), (64, True, False)])
-def test_groupnorm_fwd_bwd(ctx, c, silu, two):
+@pytest.fixture(params=["group", "3pass"])
+def gn_path(request, monkeypatch):
+    """GroupNorm launch form: one block per (frame, group) in a single launch wherever the slice fits
+    the LDS (DC_GN_GROUP=-1; by default only small slices take it), or the stats / finalize / apply
+    launches (DC_GN_GROUP=0)."""
+    monkeypatch.setenv("DC_GN_GROUP", "0" if request.param == "3pass" else "-1")   # -1: no size cap
+    return request.param
+
+
+@pytest.mark.parametrize("c,silu,two", [(320, True, False), (640, False, False), (960, True, True), (64, True, False),
+                                        (1280, True, False)])
+def test_groupnorm_fwd_bwd(ctx, gn_path, c, silu, two):
     from depth_completion_amd import ops
     n, h, w = 2, 9, 12
     x = rnd(n, c, h, w, seed=22) * 2 + 0.5
@@ -179,7 +189,7 @@ def test_groupnorm_fwd_bwd(ctx, c, silu, two):
 
 
 @pytest.mark.parametrize("n,h,w,c", [(1, 72, 96, 320), (3, 24, 32, 640), (8, 18, 24, 1280), (1, 1, 5, 64)])
-def test_groupnorm_many_chunks(ctx, n, h, w, c):
+def test_groupnorm_many_chunks(ctx, gn_path, n, h, w, c):
     """GroupNorm where the stats pass spans many blocks (the last-arriving block folds every chunk
     partial): statistics against torch fp32, and repeated calls bit-identical (counter reset)."""
     from depth_completion_amd import ops
@@ -202,6 +212,35 @@ def test_groupnorm_many_chunks(ctx, n, h, w, c):
     assert rel(nchw(y, n, h, w), F.silu(F.group_norm(x, 32, gamma, beta, eps=1e-5))) < 1e-2
     for y2, st2, dx2 in outs[1:]:
         assert torch.equal(y2, outs[0][0]) and torch.equal(st2, outs[0][1]) and torch.equal(dx2, outs[0][2])
+
+
+@pytest.mark.parametrize("n,h,w,c,two", [(1, 72, 96, 320, False), (2, 36, 48, 960, True), (1, 9, 12, 2560, True)])
+def test_groupnorm_paths_agree(ctx, monkeypatch, n, h, w, c, two):
+    """The single-launch and 3-launch GroupNorm give the same statistics (fp64 folds of fp32 partials in
+    different orders: rel 1e-5) and outputs within a bf16 ulp's worth of rounding flips."""
+    from depth_completion_amd import ops
+    x = (rnd(n, c, h, w, seed=43) * 1.5 + 0.2).to(torch.bfloat16)
+    gamma = (1 + 0.1 * rnd(c, seed=44)).to(torch.bfloat16).float()
+    beta = (0.1 * rnd(c, seed=45)).to(torch.bfloat16).float()
+    xs = nhwc(x)
+    c1 = c // 3 * 2 // 8 * 8 if two else 0
+    xa, xb = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if two else (xs, None)
+    gy = nhwc(rnd(n, c, h, w, seed=46).to(torch.bfloat16))
+    res = {}
+    for path in ("group", "3pass"):
+        monkeypatch.setenv("DC_GN_GROUP", "0" if path == "3pass" else "-1")
+        y = torch.empty_like(xs)
+        stats = torch.empty(n, 32, 2, device=dev)
+        dx = torch.empty_like(xs)
+        kw = dict(x2=xb, c1=c1) if two else {}
+        ops.groupnorm(ctx, xa, n, h * w, c, gamma, beta, 1e-6, True, y, stats, **kw)
+        ops.groupnorm_bwd(ctx, xa, n, h * w, c, gamma, beta, True, stats, gy, dx, **kw)
+        torch.cuda.synchronize()
+        res[path] = (y.float(), stats.clone(), dx.float())
+    (y1, s1, d1), (y2, s2, d2) = res["group"], res["3pass"]
+    assert rel(s1, s2) < 1e-5
+    assert rel(y1, y2) < 2e-3
+    assert rel(d1, d2) < 5e-3
 
 
 @pytest.mark.parametrize("c", [64, 320, 1280])

@@ -1,11 +1,15 @@
-"""GroupNorm(+SiLU) fwd / bwd timing at the UNet shapes (GPU)."""
+"""GroupNorm(+SiLU) fwd / bwd timing at the UNet shapes (GPU), single-launch (group) and 3-launch forms."""
+import os
 import sys
 import torch
 sys.path.insert(0, ".")
 from depth_completion_amd import ops  # noqa: E402
 from depth_completion_amd.ops import Ctx  # noqa: E402
 dev = torch.device("cuda:0"); ctx = Ctx(dev)
-for nb, hw, c in [(1, 6912, 320), (1, 6912, 640), (1, 1728, 640), (1, 432, 1280), (1, 108, 2560), (8, 6912, 320)]:
+shapes = [(1, 6912, 320), (1, 6912, 640), (1, 6912, 960), (1, 1728, 640), (1, 1728, 1280), (1, 1728, 1920),
+          (1, 432, 1280), (1, 432, 2560), (1, 108, 1280), (1, 108, 2560), (8, 6912, 320), (8, 432, 1280)]
+for (nb, hw, c), path in [(sh, p) for sh in shapes for p in ("3pass", "group")]:
+    os.environ["DC_GN_GROUP"] = "0" if path == "3pass" else "-1"
     x = torch.randn(nb * hw, c, device=dev).to(torch.bfloat16)
     g, b = torch.ones(c, device=dev), torch.zeros(c, device=dev)
     y = torch.empty_like(x); st = torch.empty(nb, 32, 2, device=dev); dy = torch.randn_like(x); dx = torch.empty_like(x)
@@ -24,4 +28,4 @@ for nb, hw, c in [(1, 6912, 320), (1, 6912, 640), (1, 1728, 640), (1, 432, 1280)
         e0.record()
         for _ in range(5): g_.replay()
         e1.record(); torch.cuda.synchronize()
-        print(f"nb={nb} hw={hw} C={c} {name}: {e0.elapsed_time(e1) / 100 * 1e3:.1f} us (graph)", flush=True)
+        print(f"nb={nb} hw={hw} C={c} {path:5s} {name}: {e0.elapsed_time(e1) / 100 * 1e3:.1f} us (graph)", flush=True)
