@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -77,6 +77,9 @@ _SIGS = {
     "dc_dense_loss_ws_bytes": [i32, i32, i32],
     "dc_guide_map": [vp, vp, vp, i32, i32, i32, vp, vp],
     "dc_dense_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp],
+    "dc_closed_form_stats": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
+    "dc_closed_form_adjoint": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp],
+    "dc_affine_step": [i32, vp, i32, f32, i32, vp, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],
     "dc_latent_scale_fwd": [vp, i32, i64, f32, vp, vp],
     "dc_latent_scale_bwd": [vp, i32, i64, f32, vp, vp, vp, vp, vp],

@@ -1106,7 +1106,7 @@ int attn_cfg(int t, int heads, int nb, bool bwd) {
   const char* e = getenv("DC_ATTN_CFG");  // read per launch (host-side, once per captured graph node)
   const int forced = e ? atoi(e) : -1;
   const int ncfg = bwd ? kNumBwdCfgs : kNumAttnCfgs;
-  if (forced >= 0 && forced < ncfg) return forced;
+  if (forced >= 0 && forced < (bwd ? kNumBwdCfgs + 1 : kNumAttnCfgs)) return forced;
   int best = 0;
   double best_t = 1e30;
   for (int i = 0; i < ncfg; ++i) {

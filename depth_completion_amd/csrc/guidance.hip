@@ -539,9 +539,11 @@ __global__ void ddim_step_kernel(bf16* x8, const bf16* v, long total, const floa
 // compute_affine_params (marigold_dc.py:53-128) over the sparse pixels only (the mask is zero elsewhere),
 // one block per frame, with the reference's dtype placement: the affine map is bf16, so its masked sum,
 // mean, centred values, squares and variance are bf16-rounded; guides and the covariance are fp32.
+// st8 (optional): [nb][8] = (scale, shift, mean a, mean g, var + eps, count) for the differentiated
+// full-image form (dc_dense_loss flag 16, dc_closed_form_adjoint)
 __global__ void closed_form_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
                                    const int* idx, const float* gval, const int* cnt, const float* params,
-                                   float* affine) {
+                                   float* affine, float* st8) {
   __shared__ float scratch[16];
   const int n = blockIdx.x;
   const long HW = (long)H * W;
@@ -575,9 +577,94 @@ __global__ void closed_form_kernel(const bf16* out, int ldo, int PH, int PW, int
   __syncthreads();
   const float cov = block_sum(sc, scratch);
   if (threadIdx.x == 0) {
-    const float scale = cov / (float)(bf16)(var + 1e-7f);
-    affine[n * 2] = scale;
-    affine[n * 2 + 1] = mg - scale * ma;
+    const float vpe = (float)(bf16)(var + 1e-7f);
+    const float scale = cov / vpe;
+    if (affine) {
+      affine[n * 2] = scale;
+      affine[n * 2 + 1] = mg - scale * ma;
+    }
+    if (st8) {
+      float* o = st8 + n * 8;
+      o[0] = scale;
+      o[1] = mg - scale * ma;
+      o[2] = ma;
+      o[3] = mg;
+      o[4] = vpe;
+      o[5] = (float)count;
+      o[6] = 0.0f;
+      o[7] = 0.0f;
+    }
+  }
+}
+
+// The fit's share of dL/da_k for the full-image closed-form loss: dc_dense_loss (flag 16) leaves
+// grad2[n] = (Gs, E) = (sum_p dF_p (a_p - mean a), sum_p dF_p) over every pixel, whose direct term
+// s dF_p it has already scattered; the sparse pixels k add Gs (gc_k - 2 s ac_k) / (V + eps) - s E / K
+// (the same expression as sparse_loss_cf_kernel's), scattered through the resize taps.  One block per
+// frame.
+__global__ void cf_adjoint_kernel(const bf16* out, int ldo, int PH, int PW, int RH, int RW, int H, int W,
+                                  const int* idx, const float* gval, const int* cnt, const float* params,
+                                  const float* st8, const float* grad2, float* dA) {
+  const int n = blockIdx.x;
+  const long HW = (long)H * W;
+  const int count = cnt[n];
+  const int* ix = idx + n * HW;
+  const float* gv = gval + n * HW;
+  const int nearest = interp_nearest(params + n * 8);
+  const float* c = st8 + n * 8;
+  const float scale = c[0], ma = c[2], mg = c[3], vpe = c[4], K = c[5];
+  const float Gs = grad2[n * 2], E = grad2[n * 2 + 1];
+  float* dAn = dA + (long)n * PH * PW;
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
+    const int p = ix[k];
+    Taps t;
+    const float a = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, p / W, p - (p / W) * W, t, nearest);
+    const float ac = (float)(bf16)(a - ma);
+    const float gc = gv[k] - mg;
+    const float dff = (float)(bf16)(Gs * (gc - 2.0f * scale * ac) / vpe - scale * E / K);
+    if (t.ly1 == 0.0f && t.lx1 == 0.0f && t.y0 == t.y1 && t.x0 == t.x1) {
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x0], dff);
+    } else {
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x0], t.ly0 * t.lx0 * dff);
+      atomicAdd(&dAn[(long)t.y0 * PW + t.x1], t.ly0 * t.lx1 * dff);
+      atomicAdd(&dAn[(long)t.y1 * PW + t.x0], t.ly1 * t.lx0 * dff);
+      atomicAdd(&dAn[(long)t.y1 * PW + t.x1], t.ly1 * t.lx1 * dff);
+    }
+  }
+}
+
+// One optimiser step of the per-input learned affine (train_method="per-input" with full-image losses):
+// grad2 [nb][2] from dc_dense_loss, state [nb][4] (Adam m0 v0 m1 v1 / Adagrad sums in m0 m1), `it` the
+// 1-based step count; the arithmetic of affine_fit_kernel's step.  One thread per frame.
+__global__ void affine_step_kernel(int nb, const float* grad2, int it, float lr, int opt, float* state,
+                                   float* affine) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= nb) return;
+  const float s = affine[n * 2], sh = affine[n * 2 + 1];
+  const float g0 = grad2[n * 2], g1 = grad2[n * 2 + 1];
+  float* m = state + n * 4;
+  if (opt == 0) {
+    double b1p = 1.0, b2p = 1.0;
+    for (int i = 0; i < it; ++i) {
+      b1p *= 0.9;
+      b2p *= 0.999;
+    }
+    const float step_size = (float)(lr / (1.0 - b1p));
+    const float bc2s = (float)sqrt(1.0 - b2p);
+    m[0] = m[0] + 0.1f * (g0 - m[0]);
+    m[1] = m[1] * 0.999f + 0.001f * g0 * g0;
+    m[2] = m[2] + 0.1f * (g1 - m[2]);
+    m[3] = m[3] * 0.999f + 0.001f * g1 * g1;
+    affine[n * 2] = s + (-step_size) * (m[0] / (sqrtf(m[1]) / bc2s + 1e-8f));
+    affine[n * 2 + 1] = sh + (-step_size) * (m[2] / (sqrtf(m[3]) / bc2s + 1e-8f));
+  } else if (opt == 1) {
+    affine[n * 2] = s + (-lr) * g0;
+    affine[n * 2 + 1] = sh + (-lr) * g1;
+  } else {
+    m[0] = m[0] + g0 * g0;
+    m[2] = m[2] + g1 * g1;
+    affine[n * 2] = s + (-lr) * (g0 / (sqrtf(m[0]) + 1e-10f));
+    affine[n * 2 + 1] = sh + (-lr) * (g1 / (sqrtf(m[2]) + 1e-10f));
   }
 }
 
@@ -768,24 +855,33 @@ __global__ void affine_fit_kernel(const bf16* out, int ldo, int PH, int PW, int 
 //                depth space, clamp and affine into dA (resize adjoint) and per-block sums of the loss,
 //                dL/d(s^2 (max-min)) and dL/d(sh^2 min) in a fixed order
 //   dense_fold   one block per frame folds the block sums in order -> loss, d scale, d shift
-// flags: 1 l1, 2 l2, 4 edge, 8 smooth.  gray = 0.299 R + 0.587 G + 0.114 B of the uint8 image, in fp32
-// as torch forms it (uint8 * python float -> float32).
+// flags: 1 l1, 2 l2, 4 edge, 8 smooth; 16 closed-form affine (affine = dc_closed_form_stats' [nb][8],
+// d = scale a + shift; the fold leaves (Gs, E) for dc_closed_form_adjoint), 32 no clamp(0, 1) (per-input
+// training, marigold_dc.py:928-929), 64 no dA (affine-only gradient).  gray = 0.299 R + 0.587 G +
+// 0.114 B of the uint8 image, in fp32 as torch forms it (uint8 * python float -> float32).
 struct DenseCtx {
   const bf16* out;
   int ldo, PH, PW, RH, RW, H, W;
   const float* params;
   const float* affine;
+  int cf, noclamp;
 };
 
+// returns N; aff = the resized decode, F = the affine value, B = dF/daff
 __device__ __forceinline__ float dense_value(const DenseCtx& c, int n, int y, int x, float& aff, float& F, float& dNdG,
-                                             Taps& t) {
+                                             Taps& t, float& B) {
   const float* pr = c.params + n * 8;
   aff = sample_affine(c.out, c.ldo, n, c.PH, c.PW, c.RH, c.RW, c.H, c.W, y, x, t, interp_nearest(pr));
-  const float s = c.affine[n * 2], sh = c.affine[n * 2 + 1];
-  const float B = (s * s) * (pr[5] - pr[4]);
-  F = B * aff + (sh * sh) * pr[4];
+  if (c.cf) {
+    B = c.affine[n * 8];
+    F = B * aff + c.affine[n * 8 + 1];
+  } else {
+    const float s = c.affine[n * 2], sh = c.affine[n * 2 + 1];
+    B = (s * s) * (pr[5] - pr[4]);
+    F = B * aff + (sh * sh) * pr[4];
+  }
   const DSpace ds(pr);
-  return ds(fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
+  return ds(c.noclamp ? F : fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
 }
 
 __device__ __forceinline__ float gray_at(const unsigned char* img, int n, long HW, long p) {
@@ -800,14 +896,14 @@ __global__ void dense_map_kernel(DenseCtx c, float* nmap) {
   const long HW = (long)c.H * c.W;
   const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= HW) return;
-  float aff, F, dNdG;
+  float aff, F, dNdG, B;
   Taps t;
-  nmap[n * HW + p] = dense_value(c, n, (int)(p / c.W), (int)(p % c.W), aff, F, dNdG, t);
+  nmap[n * HW + p] = dense_value(c, n, (int)(p / c.W), (int)(p % c.W), aff, F, dNdG, t, B);
 }
 
 // part[n][block][3] = (loss, sum dF * aff, sum dF)
 __global__ void dense_grad_kernel(DenseCtx c, const unsigned char* img, const float* nmap, const float* gmap,
-                                  const int* cnt, int flags, float* dA, float* part) {
+                                  const int* cnt, int flags, float* dA, float* part) {  // dA null: no scatter
   __shared__ float scratch[16];
   const int n = blockIdx.y;
   const int H = c.H, W = c.W;
@@ -816,9 +912,9 @@ __global__ void dense_grad_kernel(DenseCtx c, const unsigned char* img, const fl
   float lsum = 0.0f, sdb = 0.0f, sde = 0.0f;
   if (p < HW) {
     const int y = (int)(p / W), x = (int)(p % W);
-    float aff, F, dNdG;
+    float aff, F, dNdG, B;
     Taps t;
-    const float Nv = dense_value(c, n, y, x, aff, F, dNdG, t);
+    const float Nv = dense_value(c, n, y, x, aff, F, dNdG, t, B);
     const float* nm = nmap + n * HW;
     float gN = 0.0f;
     // l1 / l2 at the sparse pixels (guide map holds NaN elsewhere)
@@ -855,13 +951,10 @@ __global__ void dense_grad_kernel(DenseCtx c, const unsigned char* img, const fl
       if (y + 1 < H) gN += pair(Nv, nm[p + W], gp, edge ? gray_at(img, n, HW, p + W) : 0.0f, icy, true);
       if (y > 0) gN -= pair(nm[p - W], Nv, edge ? gray_at(img, n, HW, p - W) : 0.0f, gp, icy, false);
     }
-    const float dF = (F >= 0.0f && F <= 1.0f) ? gN * dNdG : 0.0f;
+    const float dF = (c.noclamp || (F >= 0.0f && F <= 1.0f)) ? gN * dNdG : 0.0f;
     sdb = dF * aff;
     sde = dF;
-    if (dF != 0.0f) {
-      const float* pr = c.params + n * 8;
-      const float s = c.affine[n * 2];
-      const float B = (s * s) * (pr[5] - pr[4]);
+    if (dF != 0.0f && dA) {
       const float dff = (float)(bf16)(dF * B);
       float* dAn = dA + (long)n * c.PH * c.PW;
       if (t.ly1 == 0.0f && t.lx1 == 0.0f && t.y0 == t.y1 && t.x0 == t.x1) {
@@ -887,7 +980,7 @@ __global__ void dense_grad_kernel(DenseCtx c, const unsigned char* img, const fl
   }
 }
 
-__global__ void dense_fold_kernel(const float* part, int nblk, const float* params, const float* affine,
+__global__ void dense_fold_kernel(const float* part, int nblk, const float* params, const float* affine, int cf,
                                   float* daff_grad, float* loss) {
   __shared__ float scratch[16];
   const int n = blockIdx.x;
@@ -904,10 +997,15 @@ __global__ void dense_fold_kernel(const float* part, int nblk, const float* para
   __syncthreads();
   de = block_sum(de, scratch);
   if (threadIdx.x == 0) {
-    const float* pr = params + n * 8;
-    const float s = affine[n * 2], sh = affine[n * 2 + 1];
-    daff_grad[n * 2] = (db * (pr[5] - pr[4])) * (2.0f * s);
-    daff_grad[n * 2 + 1] = (de * pr[4]) * (2.0f * sh);
+    if (cf) {   // (Gs, E) for cf_adjoint_kernel
+      daff_grad[n * 2] = db - affine[n * 8 + 2] * de;
+      daff_grad[n * 2 + 1] = de;
+    } else {
+      const float* pr = params + n * 8;
+      const float s = affine[n * 2], sh = affine[n * 2 + 1];
+      daff_grad[n * 2] = (db * (pr[5] - pr[4])) * (2.0f * s);
+      daff_grad[n * 2 + 1] = (de * pr[4]) * (2.0f * sh);
+    }
     loss[n] = l;
   }
 }
@@ -1029,7 +1127,37 @@ extern "C" int dc_closed_form_affine(const void* dec_out, int ldo, int nb, int p
                                      float* affine, void* stream) {
   if (!dec_out || !idx || !gval || !cnt || !params || !affine || nb <= 0) return DC_ERR_ARG;
   hipLaunchKernelGGL(closed_form_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
-                     pw, rh, rw, h, w, idx, gval, cnt, params, affine);
+                     pw, rh, rw, h, w, idx, gval, cnt, params, affine, (float*)nullptr);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_closed_form_stats(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h,
+                                    int w, const int* idx, const float* gval, const int* cnt, const float* params,
+                                    float* st8, void* stream) {
+  if (!dec_out || !idx || !gval || !cnt || !params || !st8 || nb <= 0 || rh > ph || rw > pw) return DC_ERR_ARG;
+  hipLaunchKernelGGL(closed_form_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
+                     pw, rh, rw, h, w, idx, gval, cnt, params, (float*)nullptr, st8);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_closed_form_adjoint(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h,
+                                      int w, const int* idx, const float* gval, const int* cnt, const float* params,
+                                      const float* st8, const float* grad2, float* dA, void* stream) {
+  if (!dec_out || !idx || !gval || !cnt || !params || !st8 || !grad2 || !dA || nb <= 0 || rh > ph || rw > pw)
+    return DC_ERR_ARG;
+  hipLaunchKernelGGL(cf_adjoint_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, (const bf16*)dec_out, ldo, ph,
+                     pw, rh, rw, h, w, idx, gval, cnt, params, st8, grad2, dA);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_affine_step(int nb, const float* grad2, int it, float lr, int opt, float* state, float* affine,
+                              void* stream) {
+  if (nb <= 0 || !grad2 || !state || !affine || it <= 0 || opt < 0 || opt > 2) return DC_ERR_ARG;
+  hipLaunchKernelGGL(affine_step_kernel, dim3((nb + 63) / 64), dim3(64), 0, (hipStream_t)stream, nb, grad2, it, lr,
+                     opt, state, affine);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -1085,18 +1213,21 @@ extern "C" int dc_dense_loss(const void* dec_out, int ldo, int nb, int ph, int p
                              const unsigned char* imgs, const float* gmap, const int* cnt, const float* params,
                              const float* affine, int flags, float* ws, float* dA, float* daff_grad, float* loss,
                              void* stream) {
-  if (!dec_out || !gmap || !cnt || !params || !affine || !ws || !dA || !daff_grad || !loss) return DC_ERR_ARG;
-  if (nb <= 0 || rh > ph || rw > pw || h < 2 || w < 2 || flags <= 0 || flags > 15) return DC_ERR_ARG;
+  if (!dec_out || !gmap || !cnt || !params || !affine || !ws || !daff_grad || !loss) return DC_ERR_ARG;
+  if (nb <= 0 || rh > ph || rw > pw || h < 2 || w < 2 || (flags & 15) == 0 || flags > 127) return DC_ERR_ARG;
   if ((flags & 4) && !imgs) return DC_ERR_ARG;
-  const DenseCtx c{(const bf16*)dec_out, ldo, ph, pw, rh, rw, h, w, params, affine};
+  if (!(flags & 64) && !dA) return DC_ERR_ARG;
+  const DenseCtx c{(const bf16*)dec_out, ldo, ph, pw, rh, rw, h, w, params, affine, (flags >> 4) & 1, (flags >> 5) & 1};
+  const int lf = flags & 15;
+  if (flags & 64) dA = nullptr;
   const long HW = (long)h * w;
   const int nblk = (int)((HW + 255) / 256);
   float* nmap = ws;
   float* part = ws + (long)nb * HW;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(dense_map_kernel, dim3(nblk, nb), dim3(256), 0, st, c, nmap);
-  hipLaunchKernelGGL(dense_grad_kernel, dim3(nblk, nb), dim3(256), 0, st, c, imgs, nmap, gmap, cnt, flags, dA, part);
-  hipLaunchKernelGGL(dense_fold_kernel, dim3(nb), dim3(256), 0, st, part, nblk, params, affine, daff_grad, loss);
+  hipLaunchKernelGGL(dense_grad_kernel, dim3(nblk, nb), dim3(256), 0, st, c, imgs, nmap, gmap, cnt, lf, dA, part);
+  hipLaunchKernelGGL(dense_fold_kernel, dim3(nb), dim3(256), 0, st, part, nblk, params, affine, c.cf, daff_grad, loss);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

@@ -206,10 +206,6 @@ class MarigoldDepthCompletionPipeline:
         for f in loss_funcs:
             loss_flags |= _LOSS_BIT[f]
         full_loss = loss_flags != 3
-        if full_loss and (fit_affine or (guided and closed_form)):
-            raise NotImplementedError("HIP path: loss_funcs other than l1 + l2 are supported for the guided "
-                                      f"learned-affine mode only; got loss_funcs={loss_funcs} with "
-                                      f"{'closed_form' if guided else 'train_method=per-input'}")
         dev = self.device
         ctx = self.ctx
         imgs = imgs.to(dev)
@@ -266,12 +262,15 @@ class MarigoldDepthCompletionPipeline:
         # full-image losses: dense guide map + the caller's uint8 image (edge term's gray gradients)
         gmap = torch.empty(n, HWs, dtype=torch.float32, device=dev)
         img_u8 = imgs.contiguous()
-        if full_loss and guided:
+        if full_loss and (guided or fit_affine):
             _lib.call("dc_guide_map", idx.data_ptr(), gval.data_ptr(), cnt.data_ptr(), n, H, W, gmap.data_ptr(),
                       ctx.stream)
             nws = _lib.load().dc_dense_loss_ws_bytes(n, H, W)
             if st.get("dense_ws") is None or st["dense_ws"].numel() * 4 < nws:
                 st["dense_ws"] = torch.empty(-(-nws // 4), dtype=torch.float32, device=dev)
+            if st.get("cf_stats") is None:   # closed-form fit statistics and (Gs, E) / per-input gradient
+                st["cf_stats"] = torch.zeros(n, 8, dtype=torch.float32, device=dev)
+                st["cf_grad"] = torch.zeros(n, 2, dtype=torch.float32, device=dev)
 
         # ---- per-call tables
         ts = self.scheduler.timesteps(steps)
@@ -327,7 +326,16 @@ class MarigoldDepthCompletionPipeline:
         dp.forward()
         dense = torch.empty(n, 1, H, W, dtype=torch.float32, device=dev)
         cs = self._tables(st)
-        if fit_affine:   # per-input training of scale / shift on the (fixed) final decode (:911-967)
+        if fit_affine and full_loss:   # per-input with edge / smooth terms: one dense-loss pass per step
+            state = torch.zeros(n, 4, dtype=torch.float32, device=dev)
+            for it in range(1, int(train_steps) + 1):
+                _lib.call("dc_dense_loss", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["img"].data_ptr(),
+                          cs["gmap"].data_ptr(), cs["cnt"].data_ptr(), cs["params"].data_ptr(),
+                          st["affine"].data_ptr(), loss_flags | 32 | 64, st["dense_ws"].data_ptr(), None,
+                          st["cf_grad"].data_ptr(), st["loss"].data_ptr(), ctx.stream)
+                _lib.call("dc_affine_step", n, st["cf_grad"].data_ptr(), it, float(lr_scaling), opt_code,
+                          state.data_ptr(), st["affine"].data_ptr(), ctx.stream)
+        elif fit_affine:   # per-input training of scale / shift on the (fixed) final decode (:911-967)
             _lib.call("dc_affine_fit", dp.out.data_ptr(), 8, n, PH, PW, RH, RW, H, W, cs["idx"].data_ptr(),
                       cs["gval"].data_ptr(), cs["cnt"].data_ptr(), cs["params"].data_ptr(), int(train_steps),
                       float(lr_scaling), opt_code, st["affine"].data_ptr(), st["loss"].data_ptr(), ctx.stream)
@@ -397,7 +405,18 @@ class MarigoldDepthCompletionPipeline:
                       dp.tin.data_ptr(), s)
         dp.forward()                                                         # VAE decode of x0
         ops.memset(ctx, st["dA"])
-        if cs["cf"]:   # closed-form fit of the preview, differentiated (daff stays zero: no learned affine)
+        if cs["cf"] and cs["loss_flags"]:   # closed-form fit + whole-map loss, the fit differentiated too
+            geo = (8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"], cs["W"])
+            _lib.call("dc_closed_form_stats", dp.out.data_ptr(), *geo, cs["idx"].data_ptr(), cs["gval"].data_ptr(),
+                      cs["cnt"].data_ptr(), cs["params"].data_ptr(), st["cf_stats"].data_ptr(), s)
+            _lib.call("dc_dense_loss", dp.out.data_ptr(), *geo, cs["img"].data_ptr(), cs["gmap"].data_ptr(),
+                      cs["cnt"].data_ptr(), cs["params"].data_ptr(), st["cf_stats"].data_ptr(),
+                      cs["loss_flags"] | 16, st["dense_ws"].data_ptr(), st["dA"].data_ptr(),
+                      st["cf_grad"].data_ptr(), st["loss"].data_ptr(), s)
+            _lib.call("dc_closed_form_adjoint", dp.out.data_ptr(), *geo, cs["idx"].data_ptr(), cs["gval"].data_ptr(),
+                      cs["cnt"].data_ptr(), cs["params"].data_ptr(), st["cf_stats"].data_ptr(),
+                      st["cf_grad"].data_ptr(), st["dA"].data_ptr(), s)
+        elif cs["cf"]:   # closed-form fit of the preview, differentiated (daff stays zero: no learned affine)
             _lib.call("dc_sparse_loss_cf", dp.out.data_ptr(), 8, n, cs["PH"], cs["PW"], cs["RH"], cs["RW"], cs["H"],
                       cs["W"], cs["idx"].data_ptr(), cs["gval"].data_ptr(), cs["cnt"].data_ptr(),
                       cs["params"].data_ptr(), st["dA"].data_ptr(), st["loss"].data_ptr(), s)

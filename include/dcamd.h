@@ -172,15 +172,33 @@ int dc_affine_fit(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, 
                   const float* gval, const int* cnt, const float* params, int train_steps, float lr, int opt,
                   float* affine, float* loss, void* stream);
 /* compute_loss with the full-image terms (marigold_dc.py:131-245: l1, l2, edge, smooth; flags 1 | 2 | 4 | 8)
- * on the learned-affine dense map of the guided step (replaces dc_sparse_loss when loss_funcs is not
- * {l1, l2}): loss[nb], daff_grad[nb][2] and the resize-adjoint gradient added into dA [nb][ph][pw].
+ * on the dense map (replaces dc_sparse_loss when loss_funcs is not {l1, l2}): loss[nb], daff_grad[nb][2]
+ * and the resize-adjoint gradient added into dA [nb][ph][pw].
  * imgs: the caller's uint8 [nb][3][h][w] (edge: gray = 0.299 R + 0.587 G + 0.114 B); gmap: dc_guide_map;
- * ws: dc_dense_loss_ws_bytes(nb, h, w) bytes. */
+ * ws: dc_dense_loss_ws_bytes(nb, h, w) bytes.
+ * flag 16: closed-form affine (marigold_dc.py:332-336): `affine` is dc_closed_form_stats' [nb][8], the map
+ *          is scale * A + shift, daff_grad receives (Gs, E) for dc_closed_form_adjoint;
+ * flag 32: no clamp(0, 1) (the per-input loop, marigold_dc.py:927-929);
+ * flag 64: dA untouched (may be null): only loss and daff_grad (per-input training). */
 long long dc_dense_loss_ws_bytes(int nb, int h, int w);
 int dc_guide_map(const int* idx, const float* gval, const int* cnt, int nb, int h, int w, float* gmap, void* stream);
 int dc_dense_loss(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
                   const unsigned char* imgs, const float* gmap, const int* cnt, const float* params,
                   const float* affine, int flags, float* ws, float* dA, float* daff_grad, float* loss, void* stream);
+/* closed_form=True guided steps with full-image losses: the fit of the preview with its statistics
+ * st8[nb][8] = (scale, shift, mean A, mean guide, var + eps, count, 0, 0) (compute_affine_params,
+ * marigold_dc.py:53-128), and, after dc_dense_loss(flags | 16), the fit's share of dL/dA at the sparse
+ * pixels added into dA (grad2 = dc_dense_loss' daff_grad) */
+int dc_closed_form_stats(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                         const int* idx, const float* gval, const int* cnt, const float* params, float* st8,
+                         void* stream);
+int dc_closed_form_adjoint(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
+                           const int* idx, const float* gval, const int* cnt, const float* params, const float* st8,
+                           const float* grad2, float* dA, void* stream);
+/* per-input training with full-image losses: one optimiser step (opt 0 Adam, 1 SGD, 2 Adagrad; `it` the
+ * 1-based step) of affine[nb][2] from grad2[nb][2] (dc_dense_loss flags | 32 | 64), state[nb][4] zeroed
+ * before the first step (marigold_dc.py:911-967) */
+int dc_affine_step(int nb, const float* grad2, int it, float lr, int opt, float* state, float* affine, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
 
 /* ---------------------------------------------------------------- AutoencoderKL (--vae original)

@@ -163,7 +163,7 @@ def test_plain_ddim_closed_form(kw):
     assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
 
 
-def _mode_parity(args, seed, label, fitted=False):
+def _mode_parity(args, seed, label, fitted=False, d_factor=2.0):
     from depth_completion_amd.config import TINY
     from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
     n, h, w, res = 2, 48, 64, 64
@@ -189,7 +189,7 @@ def _mode_parity(args, seed, label, fitted=False):
         err_h = float(((dh - d32).abs() / rng).mean())
         err_b = float(((d16 - d32).abs() / rng).mean())
     print(f"\n{label}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
-    assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
+    assert err_h <= d_factor * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
     return pipe
 
 
@@ -277,7 +277,28 @@ def test_nearest_interp(kw):
     assert dh.unique().numel() <= 48 * 64
 
 
-def test_full_loss_modes_not_silently_approximated():
+@pytest.mark.parametrize("kw", [dict(loss_funcs=["l1", "l2", "edge", "smooth"]), dict(loss_funcs=["l2", "smooth"])])
+def test_guided_closed_form_full_image_losses(kw):
+    """closed_form=True guided steps with whole-map loss terms: the fit of the preview (compute_affine_params,
+    marigold_dc.py:332-336) is differentiated through every pixel's loss (dc_closed_form_stats ->
+    dc_dense_loss flag 16 -> dc_closed_form_adjoint).  The scale's gradient sums sign-valued edge / smooth
+    terms over every pixel, and the final closed-form fit of a flattened map is ill-conditioned: trajectories
+    diverge within a few steps (the oracle's own bf16 run reaches |d| 0.06 after 6 steps and 1.4 after 3 on
+    some seeds).  One guided step here, the latent at the usual bound and the final fitted map at 3x; the
+    gradient itself is pinned against autograd in tests/test_gpu_guidance.py."""
+    _mode_parity(dict({"norm": "const", "closed_form": True}, **kw, steps=1), 30, f"guided cf {kw}", fitted=True,
+                 d_factor=3.0)
+
+
+@pytest.mark.parametrize("kw", [dict(loss_funcs=["l1", "l2", "smooth"]), dict(loss_funcs=["l1", "edge"], opt="sgd")])
+def test_per_input_full_image_losses(kw):
+    """train_method="per-input" with whole-map loss terms: each of the train_steps optimiser steps of the
+    learned scale / shift (marigold_dc.py:911-967, unclamped map) runs dc_dense_loss + dc_affine_step."""
+    _mode_parity(dict({"norm": "minmax", "train_method": "per-input", "train_steps": 10}, **kw, steps=5), 31,
+                 f"per-input {kw}")
+
+
+def test_invalid_interp_mode():
     from depth_completion_amd.config import TINY
     from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
     cfg_o = tiny_unet_config()
@@ -286,8 +307,6 @@ def test_full_loss_modes_not_silently_approximated():
     pipe = MarigoldDepthCompletionPipeline(synthetic_state_dict(unet, 1), synthetic_taesd_state_dict(vae, 2),
                                            synthetic_text_embedding(3, 64), unet_config=TINY, device=dev)
     imgs, sparses = synth_inputs(1, 48, 64, 60, seed=9)
-    with pytest.raises(NotImplementedError):
-        pipe(imgs, sparses, 120.0, resolution=64, steps=1, closed_form=True, loss_funcs=["l1", "edge"])
     with pytest.raises(ValueError):
         pipe(imgs, sparses, 120.0, resolution=64, steps=1, interp_mode="bicubic")
 
