@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include <stdlib.h>
 #include "../../include/dcamd.h"
 
 namespace {
@@ -462,6 +463,15 @@ __global__ void attn_delta_kernel(const bf16* o, int ldo, const bf16* dout, int 
 // QW p .. QW p + QW - 1 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a
 // fixed order.  Q / dO tiles (+ lse / delta rows) stream through an LDS-DMA ring; Q is not pre-scaled
 // (the 1/8 softmax scale is folded into the exp argument and into dK at the end).
+//
+// Stream-K form (SK, batch-1 shapes whose key-blocks would leave most CUs with one 4-wave block, i.e. one
+// wave per SIMD and no MFMA / VALU overlap): G = 2 blocks per CU split the flattened (key-block, query
+// tile) space into equal ranges [b U / G, (b + 1) U / G); a block walks its range one key-block segment
+// at a time.  A key-block covered by several blocks is finished by the last to arrive: each writes its
+// partial dK/dV (sc1 stores, slot b * spb + segment), waits vmcnt(0), and one lane bumps the key-block's
+// agent-scope counter; the last arriver reads every covering block's partial back in block order (sc1
+// loads), so the sum is independent of arrival order (MI355X_MICROARCH.md hand-off table, row 1), and
+// resets the counter.
 constexpr int BWD_S = 3;
 template <int QW, int KS>
 struct DkdvLds {
@@ -471,11 +481,69 @@ struct DkdvLds {
   static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
-template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(
-    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
-    bf16* dqkv, int ldd) {
-  __shared__ __attribute__((aligned(16))) char smem[DkdvLds<QW, KS>::BYTES];
+struct AttnSK {
+  float* slab;     // [G * spb slots][QW waves][NV values][64 lanes] fp32 partials
+  int* counters;   // one per key- / query-block (global index), zero between launches
+  long U;          // units: blocks x tiles swept
+  int G, spb;      // blocks of the launch, slab slots per block
+};
+
+__device__ __forceinline__ long sk_start(const AttnSK& sk, long b) { return b * sk.U / sk.G; }
+
+// the block whose range holds unit x
+__device__ __forceinline__ long sk_block_of(const AttnSK& sk, long x) {
+  long b = x * sk.G / sk.U;
+  while (b + 1 < sk.G && sk_start(sk, b + 1) <= x) ++b;
+  while (b > 0 && sk_start(sk, b) > x) --b;
+  return b;
+}
+
+// Partial hand-off of NV accumulator values per lane for block-unit `bi` (global key- / query-block index,
+// ntile tiles) swept by this block in segment `seg`.  Returns true in the block that must write the result,
+// with v holding the ordered sum of every covering block's partial.
+template <int QW, int NV>
+__device__ __forceinline__ bool sk_handoff(const AttnSK& sk, char* smem, long bi, int ntile, int seg,
+                                           float (&v)[NV]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long b = blockIdx.x;
+  float* mine = sk.slab + (((b * sk.spb + seg) * QW + wid) * NV) * 64 + lane;
+#pragma unroll
+  for (int e = 0; e < NV; ++e) __hip_atomic_store(mine + e * 64, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long x0 = bi * ntile, x1 = x0 + ntile - 1;
+  const long bf = sk_block_of(sk, x0), bl = sk_block_of(sk, x1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int* s_last = reinterpret_cast<int*>(smem);   // the ring is idle here
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(sk.counters + bi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (int)(bl - bf);
+    if (last) __hip_atomic_store(sk.counters + bi, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_last = last;
+  }
+  __syncthreads();
+  const bool last = *s_last;
+  __syncthreads();   // the next segment's LDS-DMA may land on the flag
+  if (!last) return false;
+#pragma unroll
+  for (int e = 0; e < NV; ++e) v[e] = 0.0f;
+  for (long bb = bf; bb <= bl; ++bb) {
+    const long sg = bi - sk_start(sk, bb) / ntile;   // segment index of this block-unit in block bb
+    const float* src = sk.slab + (((bb * sk.spb + sg) * QW + wid) * NV) * 64 + lane;
+    float t[NV];
+#pragma unroll
+    for (int e = 0; e < NV; ++e) t[e] = __hip_atomic_load(src + e * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[e] += t[e];
+  }
+  return true;
+}
+
+// one key-block (kb, h, n) over query tiles [t0, t0 + tcount); SK: segment `seg` of this block's range
+template <int QW, int KS, bool SK>
+__device__ __forceinline__ void dkdv_segment(char* smem, const bf16* qkv, int ld, const bf16* dout, int lddo,
+                                             const float* lse, const float* delta, int T, int heads, bf16* dqkv,
+                                             int ldd, int kb, int h, int n, int t0, int tcount, const AttnSK& sk,
+                                             long bi, int seg) {
   constexpr int NT = 64 * QW;
   constexpr int S = BWD_S;
   constexpr int STG = DkdvLds<QW, KS>::STAGE;
@@ -483,13 +551,12 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
   const int lt = threadIdx.x - part * NT;
   char* ring = smem + part * S * STG;
-  const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
   const bf16* dob = dout + (long)n * T * lddo;
   const float* lse_b = lse + ((long)n * heads + h) * T;
   const float* del_b = delta + ((long)n * heads + h) * T;
-  const int my_k = blockIdx.x * (32 * QW) + wid * 32 + (lane & 31);
+  const int my_k = kb * (32 * QW) + wid * 32 + (lane & 31);
   const bool kok = my_k < T;
   bf16x8 kf[4], vf[4];
 #pragma unroll
@@ -503,10 +570,9 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dv[db][r] = 0.0f; dk[db][r] = 0.0f; }
 
-  const int ntiles = (T + 63) / 64;
-  const int per = (ntiles + KS - 1) / KS;
-  const int tb = part * per;
-  const int mine = max(0, min(ntiles, tb + per) - tb);
+  const int per = (tcount + KS - 1) / KS;
+  const int tb = t0 + part * per;
+  const int mine = max(0, min(t0 + tcount, tb + per) - tb);
   const __amdgpu_buffer_rsrc_t rq = buf_rsrc(base + h * 64);
   const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dob + h * 64);
   const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lse_b);
@@ -642,6 +708,27 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
         }
     }
   }
+  if constexpr (SK) {
+    const int ntq = (T + 63) / 64;
+    if (!(t0 == 0 && tcount == ntq)) {   // key-block shared with other blocks: hand off
+      float v[64];
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          v[16 * db + r] = dk[db][r];
+          v[32 + 16 * db + r] = dv[db][r];
+        }
+      if (!sk_handoff<QW, 64>(sk, smem, bi, ntq, seg, v)) return;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          dk[db][r] = v[16 * db + r];
+          dv[db][r] = v[32 + 16 * db + r];
+        }
+    }
+  }
   if (kok) {
     bf16* row = dqkv + ((long)n * T + my_k) * ldd;
 #pragma unroll
@@ -661,8 +748,45 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   }
 }
 
+// walk this block's stream-K range one block-unit segment at a time (units: nblk_units x ntile)
+template <typename F>
+__device__ __forceinline__ void sk_walk(const AttnSK& sk, int ntile, F&& seg_fn) {
+  const long b = blockIdx.x;
+  long u = sk_start(sk, b);
+  const long uend = sk_start(sk, b + 1);
+  const long first = u / ntile;
+  while (u < uend) {
+    const long bi = u / ntile;
+    const int i0 = (int)(u - bi * ntile);
+    const int i1 = (int)min((long)ntile, i0 + (uend - u));
+    seg_fn(bi, i0, i1 - i0, (int)(bi - first));
+    u += i1 - i0;
+  }
+}
+
+template <int QW, int KS, bool SK>
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(
+    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
+    bf16* dqkv, int ldd, AttnSK sk) {
+  __shared__ __attribute__((aligned(16))) char smem[DkdvLds<QW, KS>::BYTES];
+  const int ntq = (T + 63) / 64;
+  if constexpr (!SK) {
+    dkdv_segment<QW, KS, false>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, blockIdx.x, blockIdx.y,
+                                blockIdx.z, 0, ntq, sk, 0, 0);
+  } else {
+    const int nkb = (T + 32 * QW - 1) / (32 * QW);
+    sk_walk(sk, ntq, [&](long bi, int t0, int cnt, int seg) {
+      const int kb = (int)(bi % nkb);
+      const long nh = bi / nkb;
+      dkdv_segment<QW, KS, true>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, kb, (int)(nh % heads),
+                                 (int)(nh / heads), t0, cnt, sk, bi, seg);
+    });
+  }
+}
+
 // dQ: 32 QW queries per block resident; KS key-splits per block, partial dQ folded through LDS.
-// K / V tiles stream through the same LDS-DMA ring as the forward.
+// K / V tiles stream through the same LDS-DMA ring as the forward.  Stream-K form as for dK/dV, over
+// (query-block, key tile).
 template <int QW, int KS>
 struct DqLds {
   static constexpr int STAGE = 2 * TILE_B;
@@ -671,11 +795,11 @@ struct DqLds {
   static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
-template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(
-    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
-    bf16* dqkv, int ldd) {
-  __shared__ __attribute__((aligned(16))) char smem[DqLds<QW, KS>::BYTES];
+template <int QW, int KS, bool SK>
+__device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, const bf16* dout, int lddo,
+                                           const float* lse, const float* delta, int T, int heads, bf16* dqkv,
+                                           int ldd, int qbk, int h, int n, int t0, int tcount, const AttnSK& sk,
+                                           long bi, int seg) {
   constexpr int NT = 64 * QW;
   constexpr int S = BWD_S;
   constexpr int STG = DqLds<QW, KS>::STAGE;
@@ -683,10 +807,9 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
   const int lt = threadIdx.x - part * NT;
   char* ring = smem + part * S * STG;
-  const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
-  const int my_q = blockIdx.x * (32 * QW) + wid * 32 + (lane & 31);
+  const int my_q = qbk * (32 * QW) + wid * 32 + (lane & 31);
   const bool qok = my_q < T;
   bf16x8 qf[4], df[4];
 #pragma unroll
@@ -701,10 +824,9 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[db][r] = 0.0f;
-  const int ntiles = (T + 63) / 64;
-  const int per = (ntiles + KS - 1) / KS;
-  const int tb = part * per;
-  const int mine = max(0, min(ntiles, tb + per) - tb);
+  const int per = (tcount + KS - 1) / KS;
+  const int tb = t0 + part * per;
+  const int mine = max(0, min(t0 + tcount, tb + per) - tb);
   const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
   const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
   TileDma<NT> dma;
@@ -809,6 +931,21 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
         for (int r = 0; r < 16; ++r) dq[db][r] += src[(16 * db + r) * 64];
     }
   }
+  if constexpr (SK) {
+    const int ntk = (T + 63) / 64;
+    if (!(t0 == 0 && tcount == ntk)) {
+      float v[32];
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[16 * db + r] = dq[db][r];
+      if (!sk_handoff<QW, 32>(sk, smem, bi, ntk, seg, v)) return;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[db][r] = v[16 * db + r];
+    }
+  }
   if (qok) {
     bf16* row = dqkv + ((long)n * T + my_q) * ldd + h * 64;
 #pragma unroll
@@ -820,6 +957,26 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
         for (int e = 0; e < 4; ++e) a[e] = (bf16)(dq[db][4 * g2 + e] * 0.125f);
         *reinterpret_cast<bf16x4*>(row + 32 * db + 8 * g2 + 4 * hh) = a;
       }
+  }
+}
+
+template <int QW, int KS, bool SK>
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(
+    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
+    bf16* dqkv, int ldd, AttnSK sk) {
+  __shared__ __attribute__((aligned(16))) char smem[DqLds<QW, KS>::BYTES];
+  const int ntk = (T + 63) / 64;
+  if constexpr (!SK) {
+    dq_segment<QW, KS, false>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, blockIdx.x, blockIdx.y,
+                              blockIdx.z, 0, ntk, sk, 0, 0);
+  } else {
+    const int nqb = (T + 32 * QW - 1) / (32 * QW);
+    sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
+      const int qbk = (int)(bi % nqb);
+      const long nh = bi / nqb;
+      dq_segment<QW, KS, true>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, qbk, (int)(nh % heads),
+                               (int)(nh / heads), t0, cnt, sk, bi, seg);
+    });
   }
 }
 
@@ -1131,10 +1288,54 @@ template <int QW, int KS>
 void launch_bwd(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
                 int heads, int nb, bf16* dqkv, int ldd, hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse, delta,
-                     t, heads, dqkv, ldd);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse, delta, t,
-                     heads, dqkv, ldd);
+  const AttnSK none{};
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse,
+                     delta, t, heads, dqkv, ldd, none);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse,
+                     delta, t, heads, dqkv, ldd, none);
+}
+
+int device_cus() {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus[dev] = 256;
+  return cus[dev];
+}
+
+// Stream-K backward (4-wave blocks, 2 per CU) when the plain grid would leave CUs with a single 4-wave
+// block; the partial slab lives in ws, the per-block counters in its last 64 KB (shared with
+// dc_conv_gemm's, all self-resetting).  DC_ATTN_SK=0 disables it.  Returns false when it does not apply.
+constexpr long kAttnCounterBytes = 64 * 1024;
+bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
+                   int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
+  constexpr int QW = 4;
+  const char* env = getenv("DC_ATTN_SK");   // read per launch (host side, once per captured graph node)
+  if (!ws || (env && atoi(env) == 0)) return false;
+  const long units_blocks = (long)((t + 32 * QW - 1) / (32 * QW)) * heads * nb;
+  const int ntile = (t + 63) / 64;
+  const long G = 2L * device_cus();
+  const long U = units_blocks * ntile;
+  const bool forced = env && atoi(env) == 2;   // tests: take the stream-K form wherever it fits
+  // per-segment costs (K/V registers, ring prologue, partial hand-off) need >= 32 tiles per block to
+  // amortise: UNet level 0 at batch 1 (57 per block) gains 19 %, level 1 (7 per block) loses 30 %
+  if (!forced && (units_blocks >= G || U < 32 * G)) return false;
+  if (units_blocks > kAttnCounterBytes / 4 || U < 2) return false;
+  const long g = min(G, U);
+  const int spb = (int)(((U + g - 1) / g + ntile - 1) / ntile + 1);
+  if (g * spb * QW * 64L * 64 * 4 > ws_bytes - kAttnCounterBytes) return false;
+  AttnSK sk;
+  sk.slab = ws;
+  sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + (ws_bytes - kAttnCounterBytes));
+  sk.U = U;
+  sk.G = (int)g;
+  sk.spb = spb;
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, 1, true>), dim3((unsigned)g), dim3(64 * QW), 0, st, qkv, ld, dout,
+                     lddo, lse, delta, t, heads, dqkv, ldd, sk);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, 1, true>), dim3((unsigned)g), dim3(64 * QW), 0, st, qkv, ld, dout, lddo,
+                     lse, delta, t, heads, dqkv, ldd, sk);
+  return true;
 }
 }  // namespace
 
@@ -1157,7 +1358,7 @@ extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, vo
 
 extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, const void* dout, int lddo,
                            const float* lse, int nb, int t, int heads, float* delta_ws, void* dqkv, int ldd,
-                           void* stream) {
+                           float* ws, long long ws_bytes, void* stream) {
   if (!qkv || !o || !dout || !lse || !delta_ws || !dqkv || nb <= 0 || t <= 0 || heads <= 0) return DC_ERR_ARG;
   if (ld % 8 || ldo % 8 || lddo % 8 || ldd % 8 || ldd < 3 * heads * 64) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
@@ -1167,6 +1368,11 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   const bf16* q = (const bf16*)qkv;
   const bf16* d = (const bf16*)dout;
   bf16* g = (bf16*)dqkv;
+  if (launch_bwd_sk(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0,
+                    st)) {
+    DC_CHECK_LAUNCH();
+    return DC_OK;
+  }
   switch (attn_cfg(t, heads, nb, true)) {
     case 0: launch_bwd<4, 1>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
     case 1: launch_bwd<4, 2>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;

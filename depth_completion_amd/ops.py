@@ -244,7 +244,7 @@ def attn_fwd(ctx: Ctx, qkv, nb, t, heads, o, lse):
 
 def attn_bwd(ctx: Ctx, qkv, o, dout, lse, nb, t, heads, delta, dqkv):
     call("dc_attn_bwd", P(qkv), LD(qkv), P(o), LD(o), P(dout), LD(dout), lse.data_ptr(), nb, t, heads,
-         delta.data_ptr(), P(dqkv), LD(dqkv), ctx.stream)
+         delta.data_ptr(), P(dqkv), LD(dqkv), ctx.ws.data_ptr(), ctx.ws_bytes, ctx.stream)
     return dqkv
 
 

@@ -91,8 +91,10 @@ int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, const float*
  * (attn2 with the constant empty-prompt context, marigold_dc.py:463, :663-674) fused with norm2.
  */
 int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse, void* stream);
+/* ws / ws_bytes: the fp32 scratch also given to dc_conv_gemm (its last 64 KB zero-filled counters); the
+ * batch-1 shapes run a stream-K backward whose partial dK / dV / dQ slabs live there (null: plain grid) */
 int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, const void* dout, int lddo, const float* lse, int nb,
-                int t, int heads, float* delta_ws, void* dqkv, int ldd, void* stream);
+                int t, int heads, float* delta_ws, void* dqkv, int ldd, float* ws, long long ws_bytes, void* stream);
 int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps, const float* gamma,
                      const float* beta, const float* U, const float* D, const float* c0, void* y, int ldy,
                      float* stats, float* probs, void* stream);

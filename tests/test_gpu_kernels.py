@@ -295,6 +295,39 @@ def test_attention_fwd_bwd(ctx, n, t, heads, cfg, monkeypatch):
     assert rel(dq.view(n, t, 3 * C), qkv.grad) < 2e-2
 
 
+@pytest.mark.parametrize("n,t,heads", [(1, 300, 2), (2, 1000, 3), (1, 6912, 5)])
+def test_attention_bwd_stream_k(ctx, n, t, heads, monkeypatch):
+    """Stream-K backward (equal ranges of the flattened (block, tile) space over 2 blocks per CU, partials
+    summed by the last-arriving block in block order): equal to the plain grid up to fp32 summation
+    order, repeated calls bit-identical, and against fp32 SDPA.  (1, 300, 2) splits every key-block over
+    5 one-tile blocks; (1, 6912, 5) is the UNet level-0 shape the default policy sends to stream-K."""
+    from depth_completion_amd import ops
+    C = heads * 64
+    qkv = rnd(n, t, 3 * C, seed=32).to(torch.bfloat16).float().requires_grad_(True)
+    q, k, v = qkv.split(C, -1)
+    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
+    o = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
+    do = rnd(n, t, C, seed=33)
+    o.backward(do)
+    qkv_b = qkv.detach().to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
+    dob = do.to(torch.bfloat16).reshape(n * t, C)
+    ob = torch.empty(n * t, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(n, heads, t, device=dev)
+    ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
+    outs = {}
+    for mode in ("0", "2", "2b"):
+        monkeypatch.setenv("DC_ATTN_SK", mode[0])
+        dq = torch.zeros_like(qkv_b)
+        delta = torch.empty(n, heads, t, device=dev)
+        ops.attn_bwd(ctx, qkv_b, ob, dob, lse, n, t, heads, delta, dq)
+        torch.cuda.synchronize()
+        outs[mode] = dq
+    assert torch.equal(outs["2"], outs["2b"])
+    assert rel(outs["2"], outs["0"]) < 5e-3
+    assert rel(outs["2"].view(n, t, 3 * C)[..., C:], qkv.grad[..., C:]) < 2e-2
+    assert rel(outs["2"].view(n, t, 3 * C), qkv.grad) < 2e-2
+
+
 @pytest.mark.parametrize("C,heads", [(320, 5), (640, 10), (1280, 20)])
 def test_cross_attention_fold(ctx, C, heads):
     """Folded 2-key cross-attention == LN2 + attn2 (2-token context) + residual; the three UNet widths
