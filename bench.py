@@ -56,8 +56,9 @@ def workload_name(h: int, w: int, batch: int) -> str:
 
 
 def conv_flops(d) -> float:
-    """Algorithmic FLOPs of one dc_conv_gemm launch (real channels, valid taps only)."""
-    M = d.nb * d.hout * d.wout
+    """Algorithmic FLOPs of one dc_conv_gemm launch (real channels, valid taps only; a row-list launch
+    counts its rows, padding included)."""
+    M = d.nrows if d.rows else d.nb * d.hout * d.wout
     K = d.kh * d.kw * d.cin
     f = 2.0 * M * d.cout * K
     if d.mode == 2:   # transposed stride-2 gather: on average 1/4 of the taps are valid

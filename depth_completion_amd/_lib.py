@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -34,7 +34,7 @@ class ConvDesc(C.Structure):
         ("y", vp), ("ldy", i32),
         ("ws", vp), ("ws_bytes", i64),
         ("geglu", i32), ("y2", vp), ("ldy2", i32), ("aux", vp), ("ldaux", i32),
-        ("algo", i32), ("splitk", i32),
+        ("algo", i32), ("splitk", i32), ("rows", vp), ("nrows", i32),
     ]
 
 
@@ -80,6 +80,11 @@ _SIGS = {
     "dc_closed_form_stats": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
     "dc_closed_form_adjoint": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp],
     "dc_affine_step": [i32, vp, i32, f32, i32, vp, vp, vp],
+    "dc_tap_mask": [vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, vp, vp],
+    "dc_dilate_mask": [vp, i32, i32, i32, vp, vp],
+    "dc_mask_rows_ws_bytes": [i64],
+    "dc_mask_count": [vp, i64, vp, vp, vp],
+    "dc_mask_rows": [vp, i64, vp, vp, i32, vp, vp],
     "dc_memset_async": [vp, i32, i64, vp],
     "dc_latent_scale_fwd": [vp, i32, i64, f32, vp, vp],
     "dc_latent_scale_bwd": [vp, i32, i64, f32, vp, vp, vp, vp, vp],
@@ -89,7 +94,7 @@ _SIGS = {
     "dc_depth_metrics_ws_bytes": [],
     "dc_depth_metrics": [vp, vp, i64, f32, f32, vp, i32, vp, vp, vp],
 }
-_RESTYPE = {"dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64}
+_RESTYPE = {"dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64}
 
 STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}
 

@@ -16,7 +16,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libdcamd.so"
 OBJ_DIR = PKG / "build_obj"
 SOURCES = ["conv_gemm.hip", "norms.hip", "attention.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
-           "version.hip"]
+           "rowsets.hip", "version.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DC_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]

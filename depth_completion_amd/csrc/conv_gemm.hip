@@ -52,7 +52,15 @@ struct ConvGemmParams {
   int ldy2;
   const bf16* aux;
   int ldaux;
+  const int* rows;      // optional: GEMM row m computes output pixel rows[m] (sorted), nrows of them
+  long nrows;
 };
+
+// GEMM rows of the launch, and the output pixel of GEMM row m (m < conv_rows(p))
+__device__ __forceinline__ long conv_rows(const ConvGemmParams& p) {
+  return p.rows ? p.nrows : (long)p.nb * p.hout * p.wout;
+}
+__device__ __forceinline__ long conv_pix(const ConvGemmParams& p, long m) { return p.rows ? (long)p.rows[m] : m; }
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of every padded / out-of-range piece
 
@@ -190,7 +198,7 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const long hwo = (long)p.hout * p.wout;
-  const long M = (long)p.nb * hwo;
+  const long M = conv_rows(p);
   const int nkc = max(0, kc_end - kc_begin);
 
   // per-thread A-row gather tables (piece j covers tile row tid/CPR + RPI j, chunk slot tid%CPR):
@@ -210,8 +218,9 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
     const long m = m0 + row;
     vmask[j] = 0u;
     if constexpr (!SMALLC) {
-      const int n = m < M ? (int)(m / hwo) : -1;
-      const int rem = m < M ? (int)(m - (long)n * hwo) : 0;
+      const long mp = m < M ? conv_pix(p, m) : 0;
+      const int n = m < M ? (int)(mp / hwo) : -1;
+      const int rem = m < M ? (int)(mp - (long)n * hwo) : 0;
       pn[j] = n;
       poy[j] = rem / p.wout;
       pox[j] = rem - poy[j] * p.wout;
@@ -219,8 +228,9 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
     }
     int yp[3] = {0, 0, 0}, xp[3] = {0, 0, 0};
     if (m < M) {
-      const int n = (int)(m / hwo);
-      const int rem = (int)(m - (long)n * hwo);
+      const long mp = conv_pix(p, m);
+      const int n = (int)(mp / hwo);
+      const int rem = (int)(mp - (long)n * hwo);
       const int oy = rem / p.wout, ox = rem - (rem / p.wout) * p.wout;
       unsigned yv = 0u, xv = 0u;
 #pragma unroll
@@ -472,7 +482,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
   constexpr int MI = WM / 16, NJ = WN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const long M = (long)p.nb * p.hout * p.wout;
+  const long M = conv_rows(p);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
   __syncthreads();  // every wave is done reading the ring
   constexpr int LDE = WN + 8;
@@ -541,7 +551,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
     if (m >= M || c >= p.cout) continue;
     float v[8];
     load8(es + row * LDE + cg * 8, v);
-    epilogue_store(p, m, c, v, false);
+    epilogue_store(p, conv_pix(p, m), c, v, false);
   }
 }
 
@@ -713,7 +723,9 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   p.geglu = d->geglu;
   p.y2 = (bf16*)d->y2; p.ldy2 = d->ldy2;
   p.aux = (const bf16*)d->aux; p.ldaux = d->ldaux;
+  p.rows = d->rows; p.nrows = d->rows ? d->nrows : 0;
   if (p.geglu < 0 || p.geglu > 2) return DC_ERR_ARG;
+  if (p.rows && (p.nrows <= 0 || p.geglu)) return DC_ERR_ARG;
   if (p.geglu) {  // plain linear / conv output only: no residual, mask, row bias or activation
     if (p.resid || p.mask || p.rowbias || p.act || p.cout % 16) return DC_ERR_ARG;
     if (p.geglu == 1 && (!p.y2 || p.ldy2 % 8 || ((uintptr_t)p.y2 & 15))) return DC_ERR_ARG;
@@ -733,7 +745,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.mask && p.ldmask % 8 != 0) return DC_ERR_ALIGN;
   if (((uintptr_t)p.x | (uintptr_t)p.x2 | (uintptr_t)p.w | (uintptr_t)p.y) & 15) return DC_ERR_ALIGN;
   if (((uintptr_t)p.resid | (uintptr_t)p.mask) & 15) return DC_ERR_ALIGN;
-  const long M = (long)p.nb * p.hout * p.wout;
+  const long M = p.rows ? p.nrows : (long)p.nb * p.hout * p.wout;
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
   if (algo == 0 || splits == 0) {

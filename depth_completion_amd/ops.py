@@ -113,7 +113,8 @@ def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
               cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
               c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
               y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None, geglu: int = 0,
-              y2=None, aux=None):
+              y2=None, aux=None, rows=None):
+    """rows: optional (int32 tensor, count) -- compute only those output pixels (sorted row indices)."""
     d = ConvDesc()
     d.x = P(x)
     d.ldx = LD(x)
@@ -143,6 +144,10 @@ def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     d.ldaux = LD(aux)
     d.ws = ctx.ws.data_ptr() if splitk else None
     d.ws_bytes = ctx.ws_bytes if splitk else 0
+    if rows is not None:
+        d.rows, d.nrows = rows[0].data_ptr(), int(rows[1])
+        if algo is None:   # row counts vary per call: the library heuristic on nrows, not the tuned table
+            algo, nsplit = 0, 0
     if algo is None:
         algo, nsplit = ctx.choose_algo(d, y)
     d.algo = algo

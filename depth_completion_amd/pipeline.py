@@ -17,6 +17,7 @@ Deviations (documented in DESIGN.md):
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -98,6 +99,8 @@ class MarigoldDepthCompletionPipeline:
         self.scheduler = DDIMTables()
         self.empty_text_embedding = text_embedding
         self.use_graph = use_graph
+        # sparse-aware decode in the guided step (point losses, TAESD): DC_SPARSE_DECODE=0 disables it
+        self.sparse_decode = os.environ.get("DC_SPARSE_DECODE", "1") != "0"
         self._plans = {}
         self.last_loss = None
 
@@ -272,6 +275,13 @@ class MarigoldDepthCompletionPipeline:
                 st["cf_stats"] = torch.zeros(n, 8, dtype=torch.float32, device=dev)
                 st["cf_grad"] = torch.zeros(n, 2, dtype=torch.float32, device=dev)
 
+        # ---- sparse-aware decode (guided steps with the point losses read the decode only at the taps)
+        row_counts = ()
+        rows = None
+        if guided and not full_loss and self.vae_kind == "light" and self.sparse_decode:
+            rows, row_counts = self._decode_rows(st, idx, cnt, params, n, PH, PW, RH, RW, H, W)
+        dp.set_rows(rows)
+
         # ---- per-call tables
         ts = self.scheduler.timesteps(steps)
         coef = self.scheduler.coef(steps).to(dev)
@@ -293,7 +303,7 @@ class MarigoldDepthCompletionPipeline:
         if self.use_graph:
             g = st["graph"]
             gkey = (guided, guided and cf, opt_code, kld_code, float(kld_weight), steps, H, W, RH, RW, lr_latent,
-                    lr_scaling, loss_flags if full_loss else 0)
+                    lr_scaling, loss_flags if full_loss else 0, row_counts)
             if g is None or st["graph_key"] != gkey:
                 # tables are rebuilt per call at new addresses: capture against this call's buffers
                 g = torch.cuda.CUDAGraph()
@@ -321,7 +331,8 @@ class MarigoldDepthCompletionPipeline:
             for _ in range(steps):
                 step_fn(st)
 
-        # ---- final decode (marigold_dc.py:969-985)
+        # ---- final decode (marigold_dc.py:969-985): the whole map
+        dp.set_rows(None)
         self._vae_input(ops.P(ops.Slice(up.x8, 4)), P, dp)
         dp.forward()
         dense = torch.empty(n, 1, H, W, dtype=torch.float32, device=dev)
@@ -349,6 +360,40 @@ class MarigoldDepthCompletionPipeline:
         _lib.call("dc_nhwc_to_nchw", ops.P(ops.Slice(up.x8, 4)), 8, n, h * w, 4, lat.data_ptr(), ctx.stream)
         self.last_loss = st["loss"]
         return dense, lat
+
+    # sets S0..S5 of taesd.DecoderPlan.set_rows, padded to multiples of _ROW_PAD rows (fewer distinct launch
+    # shapes, hence fewer graph recaptures; padding rows repeat the last pixel, rewriting identical values)
+    _ROW_PAD = 4096
+    _ROW_KEYS = ("out", "c3", "c2", "c1", "up", "dhi")
+
+    def _decode_rows(self, st, idx, cnt, params, n, PH, PW, RH, RW, H, W):
+        """Row lists of the full-resolution decoder level for the point losses; (None, ()) when the largest
+        set covers most of the map (dense is then as fast)."""
+        ctx = self.ctx
+        total = n * PH * PW
+        if st.get("row_masks") is None or st["row_masks"].shape[1] != total:
+            st["row_masks"] = torch.empty(len(self._ROW_KEYS), total, dtype=torch.uint8, device=self.device)
+            st["row_lists"] = torch.empty(len(self._ROW_KEYS), total, dtype=torch.int32, device=self.device)
+            st["row_ws"] = torch.empty(-(-_lib.load().dc_mask_rows_ws_bytes(total) // 4), dtype=torch.int32,
+                                       device=self.device)
+            st["row_cnt"] = torch.zeros(len(self._ROW_KEYS), dtype=torch.int32, device=self.device)
+        masks, lists, ws, cntd = st["row_masks"], st["row_lists"], st["row_ws"], st["row_cnt"]
+        _lib.call("dc_tap_mask", idx.data_ptr(), cnt.data_ptr(), params.data_ptr(), n, PH, PW, RH, RW, H, W,
+                  masks[0].data_ptr(), ctx.stream)
+        for k in range(1, len(self._ROW_KEYS)):
+            _lib.call("dc_dilate_mask", masks[k - 1].data_ptr(), n, PH, PW, masks[k].data_ptr(), ctx.stream)
+        rows, counts = {}, []
+        for k, key in enumerate(self._ROW_KEYS):
+            _lib.call("dc_mask_count", masks[k].data_ptr(), total, ws.data_ptr(), cntd[k:].data_ptr(), ctx.stream)
+            c = int(cntd[k].item())
+            if k == len(self._ROW_KEYS) - 1 and c > 0.6 * total:
+                return None, ()
+            pad = min(total, -(-max(c, 1) // self._ROW_PAD) * self._ROW_PAD)
+            _lib.call("dc_mask_rows", masks[k].data_ptr(), total, ws.data_ptr(), cntd[k:].data_ptr(), pad,
+                      lists[k].data_ptr(), ctx.stream)
+            rows[key] = (lists[k], pad)
+            counts.append(pad)
+        return rows, tuple(counts)
 
     def _vae_input(self, lat_ptr, P, dp):
         """decode_prediction's VAE input from the latents at lat_ptr ([P][8] rows, 4 channels): TAESD's

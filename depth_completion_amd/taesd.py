@@ -103,6 +103,14 @@ class DecoderPlan:
         self.net, self.ctx, self.nb = net, ctx, nb
         dev = net.device
         self.saved = []
+        # sparse-aware mode (set_rows): the full-resolution convs run on row lists -- S0 the resize taps of
+        # the sparse pixels, S(k+1) = S(k) dilated by 3x3 -- keyed by launch: out S0, c3 / bfin S1,
+        # c2 / dc2 S2, c1 / dc1 S3, up / dx S4, dhi S5
+        self.rows = None
+        self._full_res_grads = []
+
+        def R(key, full):
+            return self.rows[key] if (self.rows is not None and full) else None
 
         def buf(rows, cols=CH):
             t = torch.zeros(rows, cols, dtype=BF16, device=dev)
@@ -129,9 +137,10 @@ class DecoderPlan:
 
                 def fb(cv=cv, x=x, a1=a1, a2=a2, o=o, hh=hh, ww=ww):
                     kw = dict(nb=nb, hin=hh, win=ww, cin=CH, hout=hh, wout=ww, cout=CH)
-                    ops.conv_gemm(ctx, x, cv[0].wf, bias=cv[0].bias, act=1, y=a1, **kw)
-                    ops.conv_gemm(ctx, a1, cv[1].wf, bias=cv[1].bias, act=1, y=a2, **kw)
-                    ops.conv_gemm(ctx, a2, cv[2].wf, bias=cv[2].bias, resid=x, act=1, y=o, **kw)
+                    full = (hh, ww) == (self.H, self.W)
+                    ops.conv_gemm(ctx, x, cv[0].wf, bias=cv[0].bias, act=1, y=a1, rows=R("c1", full), **kw)
+                    ops.conv_gemm(ctx, a1, cv[1].wf, bias=cv[1].bias, act=1, y=a2, rows=R("c2", full), **kw)
+                    ops.conv_gemm(ctx, a2, cv[2].wf, bias=cv[2].bias, resid=x, act=1, y=o, rows=R("c3", full), **kw)
 
                 fwd.append(fb)
                 tape.append(("block", dict(cv=cv, x=x, x_relu=x_is_relu, a1=a1, a2=a2, o=o, hw=(hh, ww))))
@@ -141,7 +150,8 @@ class DecoderPlan:
                 y = buf(nb * ho * wo)
 
                 def fu(cv=cv, x=x, y=y, hh=hh, ww=ww, ho=ho, wo=wo):
-                    ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=CH, hout=ho, wout=wo, cout=CH, mode=1, y=y)
+                    ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=CH, hout=ho, wout=wo, cout=CH, mode=1, y=y,
+                                  rows=R("up", (ho, wo) == (self.H, self.W)))
 
                 fwd.append(fu)
                 tape.append(("up_conv", dict(cv=cv, x=x, x_relu=x_is_relu, y=y, hw=(hh, ww), ohw=(ho, wo))))
@@ -154,7 +164,7 @@ class DecoderPlan:
 
         def ff(hh=hh, ww=ww):
             ops.conv_gemm(ctx, xl, net.dec_out.wf, nb=nb, hin=hh, win=ww, cin=CH, hout=hh, wout=ww, cout=3,
-                          bias=net.dec_out.bias, y=self.out)
+                          bias=net.dec_out.bias, y=self.out, rows=R("out", True))
 
         fwd.append(ff)
         self.fwd = fwd
@@ -166,7 +176,9 @@ class DecoderPlan:
 
         def bfin(dpre=dpre, hh=hh, ww=ww):
             ops.conv_gemm(ctx, self.dout, net.dec_out.wd, nb=nb, hin=hh, win=ww, cin=8, hout=hh, wout=ww, cout=CH,
-                          mask=xl if last_is_relu else None, y=dpre)
+                          mask=xl if last_is_relu else None, y=dpre, rows=R("c3", True))
+
+        self._full_res_grads.append(dpre)
 
         bwd.append(bfin)
         g = dpre  # gradient w.r.t. the (pre-activation) value feeding `x`
@@ -176,12 +188,15 @@ class DecoderPlan:
                 hh, ww = d["hw"]
                 P = nb * hh * ww
                 dc2, dc1, dx = buf(P), buf(P), buf(P)
+                if (hh, ww) == (self.H, self.W):
+                    self._full_res_grads += [dc2, dc1, dx]
 
                 def bb(cv=cv, g=g, x=x, a1=a1, a2=a2, dc2=dc2, dc1=dc1, dx=dx, hh=hh, ww=ww, xr=d["x_relu"]):
                     kw = dict(nb=nb, hin=hh, win=ww, cin=CH, hout=hh, wout=ww, cout=CH)
-                    ops.conv_gemm(ctx, g, cv[2].wd, mask=a2, y=dc2, **kw)
-                    ops.conv_gemm(ctx, dc2, cv[1].wd, mask=a1, y=dc1, **kw)
-                    ops.conv_gemm(ctx, dc1, cv[0].wd, resid=g, mask=x if xr else None, y=dx, **kw)
+                    full = (hh, ww) == (self.H, self.W)
+                    ops.conv_gemm(ctx, g, cv[2].wd, mask=a2, y=dc2, rows=R("c2", full), **kw)
+                    ops.conv_gemm(ctx, dc2, cv[1].wd, mask=a1, y=dc1, rows=R("c1", full), **kw)
+                    ops.conv_gemm(ctx, dc1, cv[0].wd, resid=g, mask=x if xr else None, y=dx, rows=R("up", full), **kw)
 
                 bwd.append(bb)
                 g = dx
@@ -191,9 +206,12 @@ class DecoderPlan:
                 ho, wo = d["ohw"]
                 dhi = buf(nb * ho * wo)
                 dlo = buf(nb * hh * ww)
+                if (ho, wo) == (self.H, self.W):
+                    self._full_res_grads.append(dhi)
 
                 def bu(cv=cv, g=g, x=x, dhi=dhi, dlo=dlo, hh=hh, ww=ww, ho=ho, wo=wo, xr=d["x_relu"]):
-                    ops.conv_gemm(ctx, g, cv.wd, nb=nb, hin=ho, win=wo, cin=CH, hout=ho, wout=wo, cout=CH, y=dhi)
+                    ops.conv_gemm(ctx, g, cv.wd, nb=nb, hin=ho, win=wo, cin=CH, hout=ho, wout=wo, cout=CH, y=dhi,
+                                  rows=R("dhi", (ho, wo) == (self.H, self.W)))
                     ops.upsample_adjoint(ctx, dhi, nb, ho, wo, CH, hh, ww, dlo, mask=x if xr else None)
 
                 bwd.append(bu)
@@ -205,6 +223,15 @@ class DecoderPlan:
 
         bwd.append(b0)
         self.bwd = bwd
+
+    def set_rows(self, rows):
+        """rows: None (dense) or {"out", "c3", "c2", "c1", "up", "dhi"} -> (int32 row list, count) for the
+        sets S0, S1, S2, S3, S4, S5 of the full-resolution level.  The gradient buffers of that level are
+        zeroed, as the sparse backward writes only inside the sets and reads its neighbours."""
+        self.rows = rows
+        if rows is not None:
+            for t in self._full_res_grads:
+                ops.memset(self.ctx, t)
 
     def forward(self):
         for f in self.fwd:

@@ -405,6 +405,11 @@ class KLPlan:
 
         return b
 
+    def set_rows(self, rows):
+        """Dense only: the decoder's GroupNorms need whole-map statistics, so no sparse-aware decode."""
+        if rows is not None:
+            raise ValueError("AutoencoderKL decoder plan has no row-list mode")
+
     def forward(self):
         for f in self.fwd:
             f()

@@ -64,6 +64,10 @@ typedef struct dc_conv_desc {
   int ldaux;
   int algo;        /* 0 = heuristic, 1..dc_conv_num_algos(): tile/ring variant (plan-time autotuned) */
   int splitk;      /* 0 = heuristic, >=1 explicit K split, -1..-4 stream-K over 256..1024 blocks (needs ws) */
+  /* optional row list: only the nrows output pixels rows[0..nrows) (sorted indices into the nb*hout*wout
+   * output rows) are computed and written; the others are left untouched (no GEGLU epilogue) */
+  const int* rows;
+  int nrows;
 } dc_conv_desc;
 
 int dc_conv_num_algos(void);
@@ -202,6 +206,21 @@ int dc_closed_form_adjoint(const void* dec_out, int ldo, int nb, int ph, int pw,
  * before the first step (marigold_dc.py:911-967) */
 int dc_affine_step(int nb, const float* grad2, int it, float lr, int opt, float* state, float* affine, void* stream);
 int dc_memset_async(void* ptr, int value, long long bytes, void* stream);
+
+/* ---------------------------------------------------------------- sparse-aware decode row sets
+ * With the point losses the guided step reads the decoded map only at the resize taps of the sparse
+ * pixels (marigold_dc.py:195-205 via _latent_to_affine's resize, :366-370); the decoder's full-resolution
+ * convs then run on row lists (dc_conv_desc.rows) of the taps' receptive fields.
+ * dc_tap_mask: byte mask [nb][ph][pw] of the taps; dc_dilate_mask: 3x3 dilation (in != out);
+ * dc_mask_count then dc_mask_rows: sorted pixel indices of a mask (count[0] of them, padded up to pad_to
+ * with the last index), ws of dc_mask_rows_ws_bytes(total) bytes. */
+int dc_tap_mask(const int* idx, const int* cnt, const float* params, int nb, int ph, int pw, int rh, int rw, int h,
+                int w, unsigned char* mask, void* stream);
+int dc_dilate_mask(const unsigned char* in, int nb, int ph, int pw, unsigned char* out, void* stream);
+long long dc_mask_rows_ws_bytes(long long total);
+int dc_mask_count(const unsigned char* mask, long long total, int* ws, int* count, void* stream);
+int dc_mask_rows(const unsigned char* mask, long long total, const int* ws, const int* count, int pad_to, int* rows,
+                 void* stream);
 
 /* ---------------------------------------------------------------- AutoencoderKL (--vae original)
  * decode_prediction's vae.decode(z / scaling_factor) (marigold_dc.py:366 via diffusers) for the 4 latent

@@ -100,6 +100,42 @@ def test_conv_upsample_mode(ctx):
         assert rel(nchw(y, n, ho, wo), ref) < 1e-2
 
 
+@pytest.mark.parametrize("mode,algo,nsplit", [(0, 3, 1), (0, 13, 2), (1, 12, 1), (0, 0, 0)])
+def test_conv_row_list(ctx, mode, algo, nsplit):
+    """dc_conv_desc.rows: only the listed output pixels are computed (bitwise the dense result at those rows
+    for the same tile / split), every other row left untouched; residual and ReLU-mask epilogues included."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    n, c, h, w = 2, 64, 24, 20
+    hin, win = (h // 2, w // 2) if mode == 1 else (h, w)
+    x = nhwc(rnd(n, c, hin, win, seed=13))
+    wt = pack_conv(rnd(c, c, 3, 3, scale=0.05, seed=14)).to(dev, torch.bfloat16)
+    b = rnd(c, seed=15)
+    res = nhwc(rnd(n, c, h, w, seed=16))
+    msk = nhwc(rnd(n, c, h, w, seed=17))
+    kw = dict(nb=n, hin=hin, win=win, cin=c, hout=h, wout=w, cout=c, mode=mode, bias=b, resid=res, mask=msk,
+              algo=algo, nsplit=nsplit)
+    dense = torch.zeros(n * h * w, c, dtype=torch.bfloat16, device=dev)
+    ops.conv_gemm(ctx, x, wt, y=dense, **kw)
+    g = torch.Generator().manual_seed(18)
+    sel = torch.randperm(n * h * w, generator=g)[:300].sort().values
+    rows = torch.zeros(4096, dtype=torch.int32)
+    rows[:300] = sel.int()
+    rows[300:] = int(sel[-1])            # padding repeats the last pixel, as the pipeline pads
+    rows = rows.to(dev)
+    sparse = torch.full((n * h * w, c), 7.0, dtype=torch.bfloat16, device=dev)
+    ops.conv_gemm(ctx, x, wt, y=sparse, rows=(rows, 4096 if algo else 300), **kw)
+    torch.cuda.synchronize()
+    sel_d = sel.to(dev)
+    if algo:
+        assert torch.equal(sparse[sel_d], dense[sel_d])
+    else:   # heuristic tile / split for 300 rows: same values up to fp32 summation order
+        assert rel(sparse[sel_d], dense[sel_d]) < 1e-2
+    keep = torch.ones(n * h * w, dtype=torch.bool, device=dev)
+    keep[sel_d] = False
+    assert bool((sparse[keep] == 7.0).all())
+
+
 @pytest.mark.parametrize("h,w", [(8, 10), (7, 9)])
 def test_conv_dgrad_modes(ctx, h, w):
     """input-gradients: stride-1 (flipped weights), stride-2 (mode 2), vs autograd."""

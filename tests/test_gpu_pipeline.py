@@ -298,6 +298,43 @@ def test_per_input_full_image_losses(kw):
                  f"per-input {kw}")
 
 
+@pytest.mark.parametrize("kw", [dict(), dict(closed_form=True)])
+def test_sparse_aware_decode(kw, monkeypatch):
+    """Guided steps with the point losses run TAESD's full-resolution layers on the receptive fields of the
+    resize taps only (dc_tap_mask / dc_dilate_mask / dc_mask_rows + row-list convs): the result matches the
+    dense decode path (DC_SPARSE_DECODE=0) and the oracle.  192x256 processing resolution, 40 points, so the
+    row sets cover ~10 % of the map."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    n, h, w, res = 1, 192, 256, 256
+    cfg_o = tiny_unet_config()
+    imgs, sparses = synth_inputs(n, h, w, 40, seed=34)
+    noise = torch.randn((1, 4, 24, 32), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
+    args = dict(kw, norm="const", steps=4, resolution=res, init_noise=noise)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
+    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
+    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DC_SPARSE_DECODE", mode)
+        pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+        out[mode] = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
+        st = pipe._plans[(1, 24, 32)]
+        assert (st["graph_key"][-1] != ()) == (mode == "1")   # the row sets were used / not used
+    torch.cuda.synchronize()
+    (dh, lh), (dd, ld_) = out["1"], out["0"]
+    lat = lambda a: float((a.float() - l32.float()).norm() / l32.float().norm())  # noqa: E731
+    err_h, _ = fitted_error(dh, d32, sparses)
+    err_b, _ = fitted_error(d16, d32, sparses)
+    print(f"\nsparse decode {kw}: HIP |d| {err_h:.5f} latent {lat(lh):.4f} | dense-decode latent {lat(ld_):.4f} | "
+          f"oracle-bf16 |d| {err_b:.5f} latent {lat(l16):.4f}")
+    # the two decode paths pick different tiles / K splits (fp32 summation order), so they drift apart as
+    # far as two bf16 executions do
+    assert float((lh.float() - ld_.float()).norm() / ld_.float().norm()) <= 2 * lat(l16) + 2e-3
+    assert err_h <= 2 * err_b + 2e-3 and lat(lh) <= 2 * lat(l16) + 2e-3
+
+
 def test_invalid_interp_mode():
     from depth_completion_amd.config import TINY
     from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
