@@ -107,9 +107,13 @@ def measure_conv_kernel(pipe, st, reps: int = 3):
         return e0.elapsed_time(e1) / reps
 
     torch.cuda.synchronize()
-    t_all = timed_graph(record)
-    n = len(descs)
-    t_rest = timed_graph(skip_conv)
+    st["dec"].set_rows(st.get("row_sets"))   # the timed calls' decode row lists (sparse-aware decode)
+    try:
+        t_all = timed_graph(record)
+        n = len(descs)
+        t_rest = timed_graph(skip_conv)
+    finally:
+        st["dec"].set_rows(None)
     flops = sum(conv_flops(d) for d in descs)
     return n, max(t_all - t_rest, 1e-6), flops
 

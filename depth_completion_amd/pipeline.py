@@ -281,6 +281,7 @@ class MarigoldDepthCompletionPipeline:
         if guided and not full_loss and self.vae_kind == "light" and self.sparse_decode:
             rows, row_counts = self._decode_rows(st, idx, cnt, params, n, PH, PW, RH, RW, H, W)
         dp.set_rows(rows)
+        st["row_sets"] = rows
 
         # ---- per-call tables
         ts = self.scheduler.timesteps(steps)
