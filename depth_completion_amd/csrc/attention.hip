@@ -989,7 +989,10 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 // [head][half][vi] so a lane's two float4 of one head are conflict-free ds_read_b128s.  When U and D
 // do not fit together (C 1280 x 20 heads: 2 x 100 KB) the second reuses the first's buffer.
 constexpr int kCrossMaxHeads = 20;  // SD2 UNet: 5 / 10 / 20 heads
-constexpr int kCrossRows = 4;
+// rows (one per wave) per block: each block stages the whole U / D tables, so the wider levels (10 / 20
+// heads, 26-102 KB per table) stage once per 8 rows (level 2: 27.2 -> 24.6 us fwd), level 0 keeps 4
+template <int MAXV>
+constexpr int kCrossRows = MAXV == 1 ? 4 : 8;
 constexpr int kCrossLdsMax = 160 * 1024;
 
 __host__ __device__ inline int cross_tab_bytes(int heads, int c) { return ((heads * c * 4 + 1023) / 1024) * 1024; }
@@ -1000,7 +1003,8 @@ __device__ __forceinline__ void cross_stage(const float* tab, int heads, int nv,
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int np = heads * nv * 2;
-  for (int j = wv; j * 64 < np; j += kCrossRows) {
+  const int nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
+  for (int j = wv; j * 64 < np; j += nw) {
     const int pc = j * 64 + lane;
     const int hd = pc / (2 * nv), rem = pc - hd * 2 * nv;
     const int half = rem >= nv ? 1 : 0, vi = rem - half * nv;
@@ -1013,13 +1017,13 @@ __device__ __forceinline__ void cross_read(const char* lds, int hd, int nv, int 
 }
 
 template <int MAXV>
-__global__ __launch_bounds__(64 * kCrossRows) void cross_fwd_kernel(const bf16* x, int ldx, long rows, int c,
+__global__ __launch_bounds__(64 * kCrossRows<MAXV>) void cross_fwd_kernel(const bf16* x, int ldx, long rows, int c,
                                                                     int heads, float eps, const float* gamma,
                                                                     const float* beta, const float* U, const float* D,
                                                                     const float* c0, bf16* y, int ldy, float* stats,
                                                                     float* probs) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const long row = (long)blockIdx.x * kCrossRows + (threadIdx.x >> 6);
+  const long row = (long)blockIdx.x * kCrossRows<MAXV> + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const bool ok = row < rows;
   const int nv = c >> 3;
@@ -1135,13 +1139,13 @@ __global__ __launch_bounds__(64 * kCrossRows) void cross_fwd_kernel(const bf16* 
 }
 
 template <int MAXV>
-__global__ __launch_bounds__(64 * kCrossRows) void cross_bwd_kernel(const bf16* x, int ldx, long rows, int c,
+__global__ __launch_bounds__(64 * kCrossRows<MAXV>) void cross_bwd_kernel(const bf16* x, int ldx, long rows, int c,
                                                                     int heads, const float* gamma, const float* U,
                                                                     const float* D, const float* stats,
                                                                     const float* probs, const bf16* dy, int lddy,
                                                                     bf16* dx, int lddx) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const long row = (long)blockIdx.x * kCrossRows + (threadIdx.x >> 6);
+  const long row = (long)blockIdx.x * kCrossRows<MAXV> + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const bool ok = row < rows;
   const int nv = c >> 3;
@@ -1388,15 +1392,14 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
     const int tb = cross_tab_bytes(heads, c);                                                  \
     const size_t lds = 2 * tb <= kCrossLdsMax ? 2 * tb : tb;                                   \
     if (tb > kCrossLdsMax) return DC_ERR_ARG;                                                  \
-    dim3 grid((unsigned)((rows + kCrossRows - 1) / kCrossRows));                               \
-    dim3 blk(64 * kCrossRows);                                                                 \
+    auto grid = [&](int r) { return dim3((unsigned)((rows + r - 1) / r)); };                  \
     hipStream_t st = (hipStream_t)stream;                                                      \
     if (nv <= 64)                                                                              \
-      hipLaunchKernelGGL(KER<1>, grid, blk, lds, st, __VA_ARGS__);                             \
+      hipLaunchKernelGGL(KER<1>, grid(kCrossRows<1>), dim3(64 * kCrossRows<1>), lds, st, __VA_ARGS__); \
     else if (nv <= 192)                                                                        \
-      hipLaunchKernelGGL(KER<3>, grid, blk, lds, st, __VA_ARGS__);                             \
+      hipLaunchKernelGGL(KER<3>, grid(kCrossRows<3>), dim3(64 * kCrossRows<3>), lds, st, __VA_ARGS__); \
     else if (nv <= 320)                                                                        \
-      hipLaunchKernelGGL(KER<5>, grid, blk, lds, st, __VA_ARGS__);                             \
+      hipLaunchKernelGGL(KER<5>, grid(kCrossRows<5>), dim3(64 * kCrossRows<5>), lds, st, __VA_ARGS__); \
     else                                                                                       \
       return DC_ERR_ARG;                                                                       \
   } while (0)
