@@ -636,7 +636,10 @@ constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 
                            {64, 128, 64, 4},   {128, 128, 64, 3}, {128, 128, 32, 3}, {128, 64, 32, 4},
                            {64, 64, 32, 4},    {256, 64, 32, 3},  {128, 128, 64, 2}, {128, 128, 32, 2},
                            {128, 64, 64, 2},   {64, 64, 64, 2},   {256, 128, 32, 2}, {128, 256, 32, 2},
-                           {256, 64, 64, 2},   {128, 32, 64, 2},  {64, 32, 64, 2}};
+                           {256, 64, 64, 2},   {128, 32, 64, 2},  {64, 32, 64, 2},
+                           // deep rings (7 / 5 k-chunks in flight) for long-K shapes on small grids, where one
+                           // block per CU is bound by the bytes it keeps in flight
+                           {64, 64, 64, 8},    {128, 64, 64, 6},  {64, 128, 64, 6}, {64, 64, 32, 8}};
 constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
 
 template <int BM, int BN, int BK, int S>
@@ -758,7 +761,8 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
 #define DC_ALGO(i) \
   case i: return launch_algo<kAlgos[i].bm, kAlgos[i].bn, kAlgos[i].bk, kAlgos[i].s>(p, M, splits, smallc, s);
     DC_ALGO(1) DC_ALGO(2) DC_ALGO(3) DC_ALGO(4) DC_ALGO(5) DC_ALGO(6) DC_ALGO(7) DC_ALGO(8) DC_ALGO(9) DC_ALGO(10)
-    DC_ALGO(11) DC_ALGO(12) DC_ALGO(13) DC_ALGO(14) DC_ALGO(15) DC_ALGO(16) DC_ALGO(17) DC_ALGO(18)
+    DC_ALGO(11) DC_ALGO(12) DC_ALGO(13) DC_ALGO(14) DC_ALGO(15) DC_ALGO(16) DC_ALGO(17) DC_ALGO(18) DC_ALGO(19)
+    DC_ALGO(20) DC_ALGO(21) DC_ALGO(22)
 #undef DC_ALGO
     default: return DC_ERR_ARG;
   }

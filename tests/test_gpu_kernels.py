@@ -431,7 +431,7 @@ def test_geglu_and_upsample_adjoint(ctx):
         assert rel(nchw(out, 2, hl, wl), x.grad) < 1e-2
 
 
-@pytest.mark.parametrize("algo", list(range(1, 19)))
+@pytest.mark.parametrize("algo", list(range(1, 23)))
 @pytest.mark.parametrize("nsplit", [1, 3, -1, -2])
 def test_conv_all_algos(ctx, algo, nsplit):
     """every tile / ring variant, split-K (nsplit > 1) and stream-K (nsplit < 0: 256 / 512 blocks over
