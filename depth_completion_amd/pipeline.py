@@ -362,8 +362,10 @@ class MarigoldDepthCompletionPipeline:
         self.last_loss = st["loss"]
         return dense, lat
 
-    # sets S0..S5 of taesd.DecoderPlan.set_rows, padded to multiples of _ROW_PAD rows (fewer distinct launch
-    # shapes, hence fewer graph recaptures; padding rows repeat the last pixel, rewriting identical values)
+    # sets S0..S5 of taesd.DecoderPlan.set_rows, each padded up to a bucket -- a multiple of
+    # max(_ROW_PAD, next_pow2(count) / 4) rows -- so that frames with similar point counts share launch
+    # shapes and replay the captured step graph instead of recapturing it (padding rows repeat the last
+    # pixel, rewriting identical values; at most ~1/4 extra rows on ~60 us of row-list convs per step)
     _ROW_PAD = 4096
     _ROW_KEYS = ("out", "c3", "c2", "c1", "up", "dhi")
 
@@ -389,7 +391,8 @@ class MarigoldDepthCompletionPipeline:
             c = int(cntd[k].item())
             if k == len(self._ROW_KEYS) - 1 and c > 0.6 * total:
                 return None, ()
-            pad = min(total, -(-max(c, 1) // self._ROW_PAD) * self._ROW_PAD)
+            gran = max(self._ROW_PAD, (1 << max(c - 1, 1).bit_length()) // 4)
+            pad = min(total, -(-max(c, 1) // gran) * gran)
             _lib.call("dc_mask_rows", masks[k].data_ptr(), total, ws.data_ptr(), cntd[k:].data_ptr(), pad,
                       lists[k].data_ptr(), ctx.stream)
             rows[key] = (lists[k], pad)
