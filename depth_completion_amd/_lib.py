@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -49,7 +49,7 @@ _SIGS = {
                          vp, i32, vp, vp],
     "dc_layernorm_fwd": [vp, i32, i64, i32, f32, vp, vp, vp, i32, vp, vp],
     "dc_layernorm_bwd": [vp, i32, i64, i32, vp, vp, vp, i32, vp, i32, vp, i32, vp],
-    "dc_attn_fwd": [vp, i32, i32, i32, i32, vp, i32, vp, vp],
+    "dc_attn_fwd": [vp, i32, i32, i32, i32, vp, i32, vp, vp, i64, vp],
     "dc_attn_bwd": [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, i32, vp, i64, vp],
     "dc_crossattn_fwd": [vp, i32, i64, i32, i32, f32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
     "dc_crossattn_bwd": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, i32, vp],

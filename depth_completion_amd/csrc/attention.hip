@@ -231,6 +231,117 @@ __device__ __forceinline__ void vm_wait_n() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+struct AttnSK {
+  float* slab;     // [G * spb slots][QW waves][NV values][64 lanes] fp32 partials
+  int* counters;   // one per key- / query-block (global index), zero between launches
+  long U;          // units: blocks x tiles swept
+  int G, spb;      // blocks of the launch, slab slots per block
+};
+
+__device__ __forceinline__ long sk_start(const AttnSK& sk, long b) { return b * sk.U / sk.G; }
+
+// the block whose range holds unit x
+__device__ __forceinline__ long sk_block_of(const AttnSK& sk, long x) {
+  long b = x * sk.G / sk.U;
+  while (b + 1 < sk.G && sk_start(sk, b + 1) <= x) ++b;
+  while (b > 0 && sk_start(sk, b) > x) --b;
+  return b;
+}
+
+// Partial hand-off of NV accumulator values per lane for block-unit `bi` (global key- / query-block index,
+// ntile tiles) swept by this block in segment `seg`.  Returns true in the block that must write the result,
+// with v holding the ordered sum of every covering block's partial.
+template <int QW, int NV, bool SUM = true>
+__device__ __forceinline__ bool sk_handoff(const AttnSK& sk, char* smem, long bi, int ntile, int seg,
+                                           float (&v)[NV]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long b = blockIdx.x;
+  float* mine = sk.slab + (((b * sk.spb + seg) * QW + wid) * NV) * 64 + lane;
+#pragma unroll
+  for (int e = 0; e < NV; ++e) __hip_atomic_store(mine + e * 64, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long x0 = bi * ntile, x1 = x0 + ntile - 1;
+  const long bf = sk_block_of(sk, x0), bl = sk_block_of(sk, x1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int* s_last = reinterpret_cast<int*>(smem);   // the ring is idle here
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(sk.counters + bi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (int)(bl - bf);
+    if (last) __hip_atomic_store(sk.counters + bi, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_last = last;
+  }
+  __syncthreads();
+  const bool last = *s_last;
+  __syncthreads();   // the next segment's LDS-DMA may land on the flag
+  if (!last) return false;
+  if constexpr (!SUM) return true;   // the caller folds the partials itself
+#pragma unroll
+  for (int e = 0; e < NV; ++e) v[e] = 0.0f;
+  for (long bb = bf; bb <= bl; ++bb) {
+    const long sg = bi - sk_start(sk, bb) / ntile;   // segment index of this block-unit in block bb
+    const float* src = sk.slab + (((bb * sk.spb + sg) * QW + wid) * NV) * 64 + lane;
+    float t[NV];
+#pragma unroll
+    for (int e = 0; e < NV; ++e) t[e] = __hip_atomic_load(src + e * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int e = 0; e < NV; ++e) v[e] += t[e];
+  }
+  return true;
+}
+
+// walk this block's stream-K range one block-unit segment at a time (units: nblk_units x ntile)
+template <typename F>
+__device__ __forceinline__ void sk_walk(const AttnSK& sk, int ntile, F&& seg_fn) {
+  const long b = blockIdx.x;
+  long u = sk_start(sk, b);
+  const long uend = sk_start(sk, b + 1);
+  const long first = u / ntile;
+  while (u < uend) {
+    const long bi = u / ntile;
+    const int i0 = (int)(u - bi * ntile);
+    const int i1 = (int)min((long)ntile, i0 + (uend - u));
+    seg_fn(bi, i0, i1 - i0, (int)(bi - first));
+    u += i1 - i0;
+  }
+}
+
+// forward hand-off: partial (m, l, O) per lane; the last arriver folds every covering block's partial in
+// block order with the online-softmax rescale (m = max, l and O scaled by exp(m_i - m))
+template <int QW>
+__device__ __forceinline__ bool sk_handoff_fwd(const AttnSK& sk, char* smem, long bi, int ntile, int seg,
+                                               float (&v)[34]) {
+  float t[34];
+#pragma unroll
+  for (int e = 0; e < 34; ++e) t[e] = v[e];
+  // publish, count, and (last arriver) gather the raw partials; the fold below replaces the plain sum
+  if (!sk_handoff<QW, 34, false>(sk, smem, bi, ntile, seg, t)) return false;
+  // sk_handoff<..., false> leaves the partials of the covering blocks unsummed: re-read them in order
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long x0 = bi * ntile, x1 = x0 + ntile - 1;
+  const long bf = sk_block_of(sk, x0), bl = sk_block_of(sk, x1);
+  bool first = true;
+  for (long bb = bf; bb <= bl; ++bb) {
+    const long sg = bi - sk_start(sk, bb) / ntile;
+    const float* src = sk.slab + (((bb * sk.spb + sg) * QW + wid) * 34) * 64 + lane;
+    float p[34];
+#pragma unroll
+    for (int e = 0; e < 34; ++e) p[e] = __hip_atomic_load(src + e * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (first) {
+#pragma unroll
+      for (int e = 0; e < 34; ++e) v[e] = p[e];
+      first = false;
+      continue;
+    }
+    const float mn = fmaxf(v[0], p[0]);
+    const float a0 = fast_exp2((v[0] - mn) * LOG2E), a1 = fast_exp2((p[0] - mn) * LOG2E);
+    v[1] = v[1] * a0 + p[1] * a1;
+#pragma unroll
+    for (int e = 2; e < 34; ++e) v[e] = v[e] * a0 + p[e] * a1;
+    v[0] = mn;
+  }
+  return true;
+}
+
 // ------------------------------------------------------------------------------ forward
 // KS key-splits per block: waves QW p .. QW p + QW - 1 sweep the p-th contiguous range of key tiles
 // for the same 32 QW queries, then the partial (m, l, O) are merged through LDS in a fixed order.
@@ -244,20 +355,19 @@ struct FwdLds {
   static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
-template <int QW, int KS>
-__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(
-    const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse) {
-  __shared__ __attribute__((aligned(16))) char smem[FwdLds<QW, KS>::BYTES];
+template <int QW, int KS, bool SK>
+__device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo,
+                                            float* lse, int qbk, int h, int n, int t0, int tcount, const AttnSK& sk,
+                                            long bi, int seg) {
   constexpr int NT = 64 * QW;
   constexpr int S = FWD_S;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
   const int lt = threadIdx.x - part * NT;
   char* ring = smem + part * S * FwdLds<QW, KS>::STAGE;
-  const int h = blockIdx.y, n = blockIdx.z;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
-  const int my_q = blockIdx.x * (32 * QW) + wid * 32 + (lane & 31);
+  const int my_q = qbk * (32 * QW) + wid * 32 + (lane & 31);
   const bool qok = my_q < T;
   bf16x8 qf[4];
 #pragma unroll
@@ -270,10 +380,9 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[db][r] = 0.0f;
 
-  const int ntiles = (T + 63) / 64;
-  const int per = (ntiles + KS - 1) / KS;
-  const int tb = part * per;
-  const int mine = max(0, min(ntiles, tb + per) - tb);
+  const int per = (tcount + KS - 1) / KS;
+  const int tb = t0 + part * per;
+  const int mine = max(0, min(t0 + tcount, tb + per) - tb);
   const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
   const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
   TileDma<NT> dma;
@@ -420,6 +529,25 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
       m = mn;
     }
   }
+  if constexpr (SK) {
+    const int ntk = (T + 63) / 64;
+    if (!(t0 == 0 && tcount == ntk)) {   // query block shared with other blocks: merge (m, l, O) in block order
+      float v[34];
+      v[0] = m;
+      v[1] = l;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[2 + 16 * db + r] = oacc[db][r];
+      if (!sk_handoff_fwd<QW>(sk, smem, bi, ntk, seg, v)) return;
+      m = v[0];
+      l = v[1];
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oacc[db][r] = v[2 + 16 * db + r];
+    }
+  }
   const float lsum = l + __shfl_xor(l, 32, 64);
   const float inv = 1.0f / lsum;
   if (qok) {
@@ -434,6 +562,26 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
         *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * g2 + 4 * hh) = v;
       }
     if (hh == 0) lse[((long)n * heads + h) * T + my_q] = m + logf(lsum);
+  }
+}
+
+
+template <int QW, int KS, bool SK>
+__global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(
+    const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse, AttnSK sk) {
+  __shared__ __attribute__((aligned(16))) char smem[FwdLds<QW, KS>::BYTES];
+  const int ntk = (T + 63) / 64;
+  if constexpr (!SK) {
+    fwd_segment<QW, KS, false>(smem, qkv, ld, T, heads, o, ldo, lse, blockIdx.x, blockIdx.y, blockIdx.z, 0, ntk, sk,
+                               0, 0);
+  } else {
+    const int nqb = (T + 32 * QW - 1) / (32 * QW);
+    sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
+      const int qbk = (int)(bi % nqb);
+      const long nh = bi / nqb;
+      fwd_segment<QW, KS, true>(smem, qkv, ld, T, heads, o, ldo, lse, qbk, (int)(nh % heads), (int)(nh / heads), t0,
+                                cnt, sk, bi, seg);
+    });
   }
 }
 
@@ -480,63 +628,6 @@ struct DkdvLds {
   static constexpr int RED = (KS - 1) * QW * 64 * 64 * 4;
   static constexpr int BYTES = RING > RED ? RING : RED;
 };
-
-struct AttnSK {
-  float* slab;     // [G * spb slots][QW waves][NV values][64 lanes] fp32 partials
-  int* counters;   // one per key- / query-block (global index), zero between launches
-  long U;          // units: blocks x tiles swept
-  int G, spb;      // blocks of the launch, slab slots per block
-};
-
-__device__ __forceinline__ long sk_start(const AttnSK& sk, long b) { return b * sk.U / sk.G; }
-
-// the block whose range holds unit x
-__device__ __forceinline__ long sk_block_of(const AttnSK& sk, long x) {
-  long b = x * sk.G / sk.U;
-  while (b + 1 < sk.G && sk_start(sk, b + 1) <= x) ++b;
-  while (b > 0 && sk_start(sk, b) > x) --b;
-  return b;
-}
-
-// Partial hand-off of NV accumulator values per lane for block-unit `bi` (global key- / query-block index,
-// ntile tiles) swept by this block in segment `seg`.  Returns true in the block that must write the result,
-// with v holding the ordered sum of every covering block's partial.
-template <int QW, int NV>
-__device__ __forceinline__ bool sk_handoff(const AttnSK& sk, char* smem, long bi, int ntile, int seg,
-                                           float (&v)[NV]) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const long b = blockIdx.x;
-  float* mine = sk.slab + (((b * sk.spb + seg) * QW + wid) * NV) * 64 + lane;
-#pragma unroll
-  for (int e = 0; e < NV; ++e) __hip_atomic_store(mine + e * 64, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const long x0 = bi * ntile, x1 = x0 + ntile - 1;
-  const long bf = sk_block_of(sk, x0), bl = sk_block_of(sk, x1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int* s_last = reinterpret_cast<int*>(smem);   // the ring is idle here
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(sk.counters + bi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (int)(bl - bf);
-    if (last) __hip_atomic_store(sk.counters + bi, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *s_last = last;
-  }
-  __syncthreads();
-  const bool last = *s_last;
-  __syncthreads();   // the next segment's LDS-DMA may land on the flag
-  if (!last) return false;
-#pragma unroll
-  for (int e = 0; e < NV; ++e) v[e] = 0.0f;
-  for (long bb = bf; bb <= bl; ++bb) {
-    const long sg = bi - sk_start(sk, bb) / ntile;   // segment index of this block-unit in block bb
-    const float* src = sk.slab + (((bb * sk.spb + sg) * QW + wid) * NV) * 64 + lane;
-    float t[NV];
-#pragma unroll
-    for (int e = 0; e < NV; ++e) t[e] = __hip_atomic_load(src + e * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int e = 0; e < NV; ++e) v[e] += t[e];
-  }
-  return true;
-}
 
 // one key-block (kb, h, n) over query tiles [t0, t0 + tcount); SK: segment `seg` of this block's range
 template <int QW, int KS, bool SK>
@@ -745,22 +836,6 @@ __device__ __forceinline__ void dkdv_segment(char* smem, const bf16* qkv, int ld
         *reinterpret_cast<bf16x4*>(row + C + h * 64 + d) = a;
         *reinterpret_cast<bf16x4*>(row + 2 * C + h * 64 + d) = b;
       }
-  }
-}
-
-// walk this block's stream-K range one block-unit segment at a time (units: nblk_units x ntile)
-template <typename F>
-__device__ __forceinline__ void sk_walk(const AttnSK& sk, int ntile, F&& seg_fn) {
-  const long b = blockIdx.x;
-  long u = sk_start(sk, b);
-  const long uend = sk_start(sk, b + 1);
-  const long first = u / ntile;
-  while (u < uend) {
-    const long bi = u / ntile;
-    const int i0 = (int)(u - bi * ntile);
-    const int i1 = (int)min((long)ntile, i0 + (uend - u));
-    seg_fn(bi, i0, i1 - i0, (int)(bi - first));
-    u += i1 - i0;
   }
 }
 
@@ -1285,7 +1360,9 @@ int attn_cfg(int t, int heads, int nb, bool bwd) {
 template <int QW, int KS>
 void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
-  hipLaunchKernelGGL((attn_fwd_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o, ldo, lse);
+  const AttnSK none{};
+  hipLaunchKernelGGL((attn_fwd_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o, ldo, lse,
+                     none);
 }
 
 template <int QW, int KS>
@@ -1312,10 +1389,10 @@ int device_cus() {
 // block; the partial slab lives in ws, the per-block counters in its last 64 KB (shared with
 // dc_conv_gemm's, all self-resetting).  DC_ATTN_SK=0 disables it.  Returns false when it does not apply.
 constexpr long kAttnCounterBytes = 64 * 1024;
-bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
-                   int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
+// stream-K plan for QW = 4 blocks (2 per CU): false when it does not apply; `env` names the switch
+bool sk_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env_name, AttnSK& sk) {
   constexpr int QW = 4;
-  const char* env = getenv("DC_ATTN_SK");   // read per launch (host side, once per captured graph node)
+  const char* env = getenv(env_name);   // read per launch (host side, once per captured graph node)
   if (!ws || (env && atoi(env) == 0)) return false;
   const long units_blocks = (long)((t + 32 * QW - 1) / (32 * QW)) * heads * nb;
   const int ntile = (t + 63) / 64;
@@ -1329,26 +1406,50 @@ bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* dout, int lddo, const fl
   const long g = min(G, U);
   const int spb = (int)(((U + g - 1) / g + ntile - 1) / ntile + 1);
   if (g * spb * QW * 64L * 64 * 4 > ws_bytes - kAttnCounterBytes) return false;
-  AttnSK sk;
   sk.slab = ws;
   sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + (ws_bytes - kAttnCounterBytes));
   sk.U = U;
   sk.G = (int)g;
   sk.spb = spb;
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, 1, true>), dim3((unsigned)g), dim3(64 * QW), 0, st, qkv, ld, dout,
-                     lddo, lse, delta, t, heads, dqkv, ldd, sk);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, 1, true>), dim3((unsigned)g), dim3(64 * QW), 0, st, qkv, ld, dout, lddo,
+  return true;
+}
+
+bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
+                   int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
+  AttnSK sk;
+  if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK", sk)) return false;
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout, lddo,
                      lse, delta, t, heads, dqkv, ldd, sk);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout, lddo,
+                     lse, delta, t, heads, dqkv, ldd, sk);
+  return true;
+}
+
+// Stream-K forward: opt-in (DC_ATTN_SK_FWD=1: the backward's policy, 2: wherever it fits).  Measured
+// neutral at level 0 (108 vs 109 us, C2 unchanged: profiles/r01r_attn_fwd_sk.txt): the forward's plain
+// (5, 2) grid already runs 10-wave blocks, and it is VALU-bound (exp) rather than occupancy-bound.
+bool launch_fwd_sk(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, float* ws,
+                   long ws_bytes, hipStream_t st) {
+  AttnSK sk;
+  const char* on = getenv("DC_ATTN_SK_FWD");
+  if (!on || atoi(on) == 0 || (getenv("DC_ATTN_SK") && atoi(getenv("DC_ATTN_SK")) == 0)) return false;
+  if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK_FWD", sk)) return false;
+  hipLaunchKernelGGL((attn_fwd_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, t, heads, o, ldo,
+                     lse, sk);
   return true;
 }
 }  // namespace
 
 extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse,
-                           void* stream) {
+                           float* ws, long long ws_bytes, void* stream) {
   if (!qkv || !o || !lse || nb <= 0 || t <= 0 || heads <= 0) return DC_ERR_ARG;
   if (ld % 8 || ldo % 8 || ld < 3 * heads * 64 || ldo < heads * 64) return DC_ERR_ALIGN;
   const bf16* q = (const bf16*)qkv;
   hipStream_t st = (hipStream_t)stream;
+  if (launch_fwd_sk(q, ld, t, heads, nb, (bf16*)o, ldo, lse, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st)) {
+    DC_CHECK_LAUNCH();
+    return DC_OK;
+  }
   switch (attn_cfg(t, heads, nb, false)) {
     case 0: launch_fwd<4, 1>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
     case 1: launch_fwd<4, 2>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;

@@ -243,7 +243,8 @@ def layernorm_bwd(ctx: Ctx, x, rows, c, gamma, stats, dy, dx, add=None):
 
 # ------------------------------------------------------------------------- attention
 def attn_fwd(ctx: Ctx, qkv, nb, t, heads, o, lse):
-    call("dc_attn_fwd", P(qkv), LD(qkv), nb, t, heads, P(o), LD(o), lse.data_ptr(), ctx.stream)
+    call("dc_attn_fwd", P(qkv), LD(qkv), nb, t, heads, P(o), LD(o), lse.data_ptr(), ctx.ws.data_ptr(), ctx.ws_bytes,
+         ctx.stream)
     return o
 
 

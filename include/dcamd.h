@@ -94,9 +94,11 @@ int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, const float*
  * Self-attention (Attention.attn1 via SDPA) fwd/bwd and the folded 2-key cross-attention
  * (attn2 with the constant empty-prompt context, marigold_dc.py:463, :663-674) fused with norm2.
  */
-int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse, void* stream);
 /* ws / ws_bytes: the fp32 scratch also given to dc_conv_gemm (its last 64 KB zero-filled counters); the
- * batch-1 shapes run a stream-K backward whose partial dK / dV / dQ slabs live there (null: plain grid) */
+ * batch-1 level-0 shapes run stream-K kernels whose partial (m, l, O) / dK / dV / dQ slabs live there
+ * (null: plain grid) */
+int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse, float* ws,
+                long long ws_bytes, void* stream);
 int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, const void* dout, int lddo, const float* lse, int nb,
                 int t, int heads, float* delta_ws, void* dqkv, int ldd, float* ws, long long ws_bytes, void* stream);
 int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps, const float* gamma,
