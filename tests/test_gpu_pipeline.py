@@ -298,18 +298,21 @@ def test_per_input_full_image_losses(kw):
                  f"per-input {kw}")
 
 
-@pytest.mark.parametrize("kw", [dict(), dict(closed_form=True)])
-def test_sparse_aware_decode(kw, monkeypatch):
+@pytest.mark.parametrize("kw,res", [(dict(), 256), (dict(closed_form=True), 256), (dict(), 192),
+                                    (dict(interp_mode="nearest"), 192)])
+def test_sparse_aware_decode(kw, res, monkeypatch):
     """Guided steps with the point losses run TAESD's full-resolution layers on the receptive fields of the
     resize taps only (dc_tap_mask / dc_dilate_mask / dc_mask_rows + row-list convs): the result matches the
-    dense decode path (DC_SPARSE_DECODE=0) and the oracle.  192x256 processing resolution, 40 points, so the
-    row sets cover ~10 % of the map."""
+    dense decode path (DC_SPARSE_DECODE=0) and the oracle.  192x256 images, 40 points: at resolution 256
+    the taps are the sparse pixels themselves; at 192 the 144x192 decode is resized up to 192x256, so the
+    tap sets come from the bilinear (4 taps) or nearest (1 tap) source rule."""
     from depth_completion_amd.config import TINY
     from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
-    n, h, w, res = 1, 192, 256, 256
+    n, h, w = 1, 192, 256
+    ph, pw = -(-(res * h // max(h, w)) // 8) * 8, -(-(res * w // max(h, w)) // 8) * 8
     cfg_o = tiny_unet_config()
     imgs, sparses = synth_inputs(n, h, w, 40, seed=34)
-    noise = torch.randn((1, 4, 24, 32), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
+    noise = torch.randn((1, 4, ph // 8, pw // 8), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
     args = dict(kw, norm="const", steps=4, resolution=res, init_noise=noise)
     o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
     d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
@@ -320,7 +323,7 @@ def test_sparse_aware_decode(kw, monkeypatch):
         monkeypatch.setenv("DC_SPARSE_DECODE", mode)
         pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
         out[mode] = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
-        st = pipe._plans[(1, 24, 32)]
+        st = pipe._plans[(1, ph // 8, pw // 8)]
         assert (st["graph_key"][-1] != ()) == (mode == "1")   # the row sets were used / not used
     torch.cuda.synchronize()
     (dh, lh), (dd, ld_) = out["1"], out["0"]
