@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -66,7 +66,8 @@ _SIGS = {
     "dc_preview": [vp, vp, i32, i32, vp, vp, vp, vp, vp, vp],
     "dc_sparse_loss": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp],
     "dc_decode_tail_bwd": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp],
-    "dc_latent_update": [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp],
+    "dc_latent_update": [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp, i64,
+                         vp],
     "dc_step_advance": [vp, i32, vp],
     "dc_latent_init": [vp, vp, f32, i32, i32, vp, vp],
     "dc_final_dense": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp],

@@ -16,6 +16,7 @@
 // Elementwise arithmetic mirrors PyTorch's op-by-op rounding (bf16 results of bf16 ops, fp32 for
 // the affine/loss), so the only deviation from the reference is reduction order.
 #include "common.h"
+#include <stdlib.h>
 #include "../../include/dcamd.h"
 
 #pragma clang fp contract(off)
@@ -359,6 +360,74 @@ struct Kld {
   }
 };
 
+// Per-element second pass of the latent update (rescaled gradient g): Adam / SGD / Adagrad with torch's
+// bf16 rounding per op, then the DDIM prev-sample with the pre-update v.
+struct UpdCtx {
+  float sa, sb, sap, sbp, step_size, bc2s, step_aff;
+  int opt;
+};
+__device__ __forceinline__ void latent_elem_update(const UpdCtx& u, bf16* x8, const bf16* v, bf16* m_lat, bf16* v_lat,
+                                                   long pix, int k, float g) {
+  const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
+  const float sa = u.sa, sb = u.sb, sap = u.sap, sbp = u.sbp, step_size = u.step_size, bc2s = u.bc2s;
+  const int opt = u.opt;
+  const long e = pix * 4 + k;
+  const float x = (float)x8[pix * 8 + 4 + k];
+  float xp;
+  if (opt == 0) {
+    float m = (float)m_lat[e], vv = (float)v_lat[e];
+    m = (float)(bf16)(m + beta1w * (g - m));
+    vv = (float)(bf16)(vv * beta2);
+    vv = (float)(bf16)(vv + one_m_b2 * g * g);
+    m_lat[e] = (bf16)m;
+    v_lat[e] = (bf16)vv;
+    float den = (float)(bf16)sqrtf(vv);
+    den = (float)(bf16)(den / bc2s);
+    den = (float)(bf16)(den + eps);
+    xp = (float)(bf16)(x + (-step_size) * (m / den));
+  } else if (opt == 1) {
+    xp = (float)(bf16)(x + (-step_size) * g);
+  } else {
+    float sum = (float)(bf16)((float)m_lat[e] + g * g);
+    m_lat[e] = (bf16)sum;
+    const float sd = (float)(bf16)((float)(bf16)sqrtf(sum) + 1e-10f);
+    xp = (float)(bf16)(x + (-step_size) * (g / sd));
+  }
+  const float vm = (float)v[pix * 8 + k];
+  const float x0 = (float)(bf16)((float)(bf16)(sa * xp) - (float)(bf16)(sb * vm));
+  const float ep = (float)(bf16)((float)(bf16)(sa * vm) + (float)(bf16)(sb * xp));
+  const float dir = (float)(bf16)(sbp * ep);
+  const float prev = (float)(bf16)((float)(bf16)(sap * x0) + dir);
+  x8[pix * 8 + 4 + k] = (bf16)prev;
+}
+
+// the same rule on scale (j = 0) / shift (j = 1), fp32 state
+__device__ __forceinline__ void affine_update(const UpdCtx& u, int n, int j, const float* daff_grad, float* affine,
+                                              float* m_aff, float* v_aff) {
+  const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
+  const int opt = u.opt;
+  const float step_aff = u.step_aff, bc2s = u.bc2s;
+  const float g = daff_grad[n * 2 + j];
+  if (opt == 0) {
+    float m = m_aff[n * 2 + j], vv = v_aff[n * 2 + j];
+    m = m + beta1w * (g - m);
+    vv = vv * beta2;
+    vv = vv + one_m_b2 * g * g;
+    m_aff[n * 2 + j] = m;
+    v_aff[n * 2 + j] = vv;
+    float den = sqrtf(vv);
+    den = den / bc2s;
+    den = den + eps;
+    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (m / den);
+  } else if (opt == 1) {
+    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * g;
+  } else {
+    const float sum = m_aff[n * 2 + j] + g * g;
+    m_aff[n * 2 + j] = sum;
+    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (g / (sqrtf(sum) + 1e-10f));
+  }
+}
+
 // opt: 0 Adam (bf16 state m_lat / v_lat), 1 SGD (no state), 2 Adagrad (bf16 state sum in m_lat); the
 // affine scalars take the same rule in fp32.  tab per step: Adam [lr_lat/bc1, sqrt(bc2), lr_aff/bc1, 0],
 // SGD / Adagrad [lr_lat, 0, lr_aff, 0].
@@ -372,7 +441,6 @@ __global__ void latent_update_kernel(bf16* x8, const bf16* v, const bf16* gdir, 
   const int st = *step;
   const float sa = coef[st * 4 + 0], sb = coef[st * 4 + 1], sap = coef[st * 4 + 2], sbp = coef[st * 4 + 3];
   const float step_size = adam_tab[st * 4 + 0], bc2s = adam_tab[st * 4 + 1], step_aff = adam_tab[st * 4 + 2];
-  const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
   Kld kl{kld_mode, kld_weight, 0.0f, 1.0f, 1.0f / (4.0f * hw)};
   if (kld_mode == 2) {  // mean / biased variance of the latent (bf16 reductions)
     float s1 = 0.0f;
@@ -406,64 +474,80 @@ __global__ void latent_update_kernel(bf16* x8, const bf16* v, const bf16* gdir, 
   const float gnc = gn < 1e-7f ? (float)(bf16)1e-7f : gn;
   const float factor = (float)(bf16)(en / gnc);
   // pass 2: rescale, Adam (bf16 state), DDIM update with the pre-update v
+  const UpdCtx u{sa, sb, sap, sbp, step_size, bc2s, step_aff, opt};
   for (int i = threadIdx.x; i < hw * 4; i += blockDim.x) {
     const long pix = (long)n * hw + (i >> 2);
     const int k = i & 3;
-    const long e = pix * 4 + k;
-    float g = grad_at(pix, k);
-    g = (float)(bf16)(g * factor);
-    const float x = (float)x8[pix * 8 + 4 + k];
-    float xp;
-    if (opt == 0) {
-      float m = (float)m_lat[e], vv = (float)v_lat[e];
-      m = (float)(bf16)(m + beta1w * (g - m));
-      vv = (float)(bf16)(vv * beta2);
-      vv = (float)(bf16)(vv + one_m_b2 * g * g);
-      m_lat[e] = (bf16)m;
-      v_lat[e] = (bf16)vv;
-      float den = (float)(bf16)sqrtf(vv);
-      den = (float)(bf16)(den / bc2s);
-      den = (float)(bf16)(den + eps);
-      xp = (float)(bf16)(x + (-step_size) * (m / den));
-    } else if (opt == 1) {
-      xp = (float)(bf16)(x + (-step_size) * g);
-    } else {
-      float sum = (float)(bf16)((float)m_lat[e] + g * g);
-      m_lat[e] = (bf16)sum;
-      const float sd = (float)(bf16)((float)(bf16)sqrtf(sum) + 1e-10f);
-      xp = (float)(bf16)(x + (-step_size) * (g / sd));
-    }
-    const float vm = (float)v[pix * 8 + k];
-    const float x0 = (float)(bf16)((float)(bf16)(sa * xp) - (float)(bf16)(sb * vm));
-    const float ep = (float)(bf16)((float)(bf16)(sa * vm) + (float)(bf16)(sb * xp));
-    const float dir = (float)(bf16)(sbp * ep);
-    const float prev = (float)(bf16)((float)(bf16)(sap * x0) + dir);
-    x8[pix * 8 + 4 + k] = (bf16)prev;
+    latent_elem_update(u, x8, v, m_lat, v_lat, pix, k, (float)(bf16)(grad_at(pix, k) * factor));
   }
-  if (threadIdx.x < 2) {
-    // the same rule on scale (0) / shift (1), fp32 state
-    const int j = threadIdx.x;
-    const float g = daff_grad[n * 2 + j];
-    if (opt == 0) {
-      float m = m_aff[n * 2 + j], vv = v_aff[n * 2 + j];
-      m = m + beta1w * (g - m);
-      vv = vv * beta2;
-      vv = vv + one_m_b2 * g * g;
-      m_aff[n * 2 + j] = m;
-      v_aff[n * 2 + j] = vv;
-      float den = sqrtf(vv);
-      den = den / bc2s;
-      den = den + eps;
-      affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (m / den);
-    } else if (opt == 1) {
-      affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * g;
-    } else {
-      const float sum = m_aff[n * 2 + j] + g * g;
-      m_aff[n * 2 + j] = sum;
-      affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (g / (sqrtf(sum) + 1e-10f));
-    }
-  }
+  if (threadIdx.x < 2) affine_update(u, n, threadIdx.x, daff_grad, affine, m_aff, v_aff);
   if (dbg && threadIdx.x == 0) {
+    dbg[n * 4 + 0] = gn;
+    dbg[n * 4 + 1] = factor;
+  }
+}
+
+// Split form of latent_update_kernel (kld_mode 0 / 1, the common case): the single-block update was
+// latency-bound at 64 us per step (27 648 scattered 2-B loads per frame through one CU).  Pass 1 gives
+// per-block partial sums of g^2, one pixel (4 channels, 8-B loads) per thread; pass 2 folds the frame's
+// partials in a fixed order (lane-strided sums + a fixed shuffle tree: deterministic) and applies the
+// update to its own pixels.
+__global__ void latent_norm_kernel(const bf16* x8, const bf16* gdir, const bf16* gunet, int hw, int kld_mode,
+                                   float kld_weight, float* part) {
+  __shared__ float scratch[16];
+  const int n = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const Kld kl{kld_mode, kld_weight, 0.0f, 1.0f, 1.0f / (4.0f * hw)};
+  float ss = 0.0f;
+  if (p < hw) {
+    const long pix = (long)n * hw + p;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float g = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
+      if (kld_mode) g = (float)(bf16)(g + kl.grad((float)x8[pix * 8 + 4 + k]));
+      ss += g * g;
+    }
+  }
+  const float t = block_sum(ss, scratch);
+  if (threadIdx.x == 0) part[(long)n * gridDim.x + blockIdx.x] = t;
+}
+
+__global__ void latent_apply_kernel(bf16* x8, const bf16* v, const bf16* gdir, const bf16* gunet, int hw,
+                                    const float* coef, const float* adam_tab, const int* step, const float* eps_norm,
+                                    bf16* m_lat, bf16* v_lat, float* affine, float* m_aff, float* v_aff,
+                                    const float* daff_grad, float* dbg, int opt, int kld_mode, float kld_weight,
+                                    const float* part) {
+  __shared__ float s_ss;
+  const int n = blockIdx.y, nblk = gridDim.x;
+  if (threadIdx.x < 64) {
+    float t = 0.0f;
+    for (int b = threadIdx.x; b < nblk; b += 64) t += part[(long)n * nblk + b];
+    t = wave_sum(t);
+    if (threadIdx.x == 0) s_ss = t;
+  }
+  __syncthreads();
+  const int st = *step;
+  const UpdCtx u{coef[st * 4 + 0], coef[st * 4 + 1], coef[st * 4 + 2], coef[st * 4 + 3], adam_tab[st * 4 + 0],
+                 adam_tab[st * 4 + 1], adam_tab[st * 4 + 2], opt};
+  const float gn = (float)(bf16)sqrtf(s_ss);
+  const float en = eps_norm[n];
+  const float gnc = gn < 1e-7f ? (float)(bf16)1e-7f : gn;
+  const float factor = (float)(bf16)(en / gnc);
+  const Kld kl{kld_mode, kld_weight, 0.0f, 1.0f, 1.0f / (4.0f * hw)};
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < hw) {
+    const long pix = (long)n * hw + p;
+    float g[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // all reads of x before the in-place update of this pixel
+      g[k] = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
+      if (kld_mode) g[k] = (float)(bf16)(g[k] + kl.grad((float)x8[pix * 8 + 4 + k]));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) latent_elem_update(u, x8, v, m_lat, v_lat, pix, k, (float)(bf16)(g[k] * factor));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2) affine_update(u, n, threadIdx.x, daff_grad, affine, m_aff, v_aff);
+  if (dbg && blockIdx.x == 0 && threadIdx.x == 0) {
     dbg[n * 4 + 0] = gn;
     dbg[n * 4 + 1] = factor;
   }
@@ -1076,10 +1160,22 @@ extern "C" int dc_latent_update(void* x8, const void* v, const void* gdir, const
                                 const float* coef, const float* adam_tab, const int* step, const float* eps_norm,
                                 void* m_lat, void* v_lat, float* affine, float* m_aff, float* v_aff,
                                 const float* daff_grad, float* dbg, int opt, int kld_mode, float kld_weight,
-                                void* stream) {
+                                float* ws, long long ws_bytes, void* stream) {
   if (!x8 || !v || !gdir || !gunet || !coef || !adam_tab || !step || !eps_norm || !m_lat || !v_lat || !affine ||
       !m_aff || !v_aff || !daff_grad || nb <= 0 || hw <= 0 || opt < 0 || opt > 2 || kld_mode < 0 || kld_mode > 2)
     return DC_ERR_ARG;
+  const int nblk = (hw + 255) / 256;
+  const char* split_env = getenv("DC_LU_SPLIT");   // 0: the single-block form (A/B)
+  if (ws && kld_mode != 2 && (long long)nb * nblk * 4 <= ws_bytes && !(split_env && atoi(split_env) == 0)) {
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(latent_norm_kernel, dim3(nblk, nb), dim3(256), 0, st, (const bf16*)x8, (const bf16*)gdir,
+                       (const bf16*)gunet, hw, kld_mode, kld_weight, ws);
+    hipLaunchKernelGGL(latent_apply_kernel, dim3(nblk, nb), dim3(256), 0, st, (bf16*)x8, (const bf16*)v,
+                       (const bf16*)gdir, (const bf16*)gunet, hw, coef, adam_tab, step, eps_norm, (bf16*)m_lat,
+                       (bf16*)v_lat, affine, m_aff, v_aff, daff_grad, dbg, opt, kld_mode, kld_weight, ws);
+    DC_CHECK_LAUNCH();
+    return DC_OK;
+  }
   hipLaunchKernelGGL(latent_update_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, (bf16*)x8, (const bf16*)v,
                      (const bf16*)gdir, (const bf16*)gunet, hw, coef, adam_tab, step, eps_norm, (bf16*)m_lat,
                      (bf16*)v_lat, affine, m_aff, v_aff, daff_grad, dbg, opt, kld_mode, kld_weight);

@@ -493,5 +493,5 @@ class MarigoldDepthCompletionPipeline:
                   h * w, cs["coef"].data_ptr(), cs["adam"].data_ptr(), step, st["eps_norm"].data_ptr(),
                   st["m_lat"].data_ptr(), st["v_lat"].data_ptr(), st["affine"].data_ptr(), st["m_aff"].data_ptr(),
                   st["v_aff"].data_ptr(), st["daff"].data_ptr(), st["dbg"].data_ptr(), cs["opt"], cs["kld"],
-                  cs["kld_weight"], s)
+                  cs["kld_weight"], ctx.ws.data_ptr(), ctx.ws_bytes, s)
         _lib.call("dc_step_advance", step, int(cs["coef"].shape[0]), s)

@@ -157,7 +157,9 @@ int dc_decode_tail_bwd(const void* dec_out, int ldo, const float* dA, int nb, in
 int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gunet, int nb, int hw, const float* coef,
                      const float* adam_tab, const int* step, const float* eps_norm, void* m_lat, void* v_lat,
                      float* affine, float* m_aff, float* v_aff, const float* daff_grad, float* dbg, int opt,
-                     int kld_mode, float kld_weight, void* stream);
+                     int kld_mode, float kld_weight, float* ws, long long ws_bytes, void* stream);
+/* ws (nb * ceil(hw / 256) floats; may be null): per-block partials of ||g||^2 for the two-launch form
+ * (kld_mode 0 / 1); without it (or with the strict KL term) one block per frame does both passes */
 int dc_step_advance(int* step, int nsteps, void* stream);  /* saturates at nsteps-1 */
 int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8, void* stream);
 int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
