@@ -160,28 +160,6 @@ __global__ void gn_apply_kernel(GNShape s, const float* stats, const float* gamm
 }
 
 // dy' = dy * silu'(y) (y = gn(x) rounded to bf16, dy' rounded to bf16), as autograd does on bf16
-__device__ __forceinline__ void gn_bwd_elem(const GNShape& s, int n, int row, int cg, const float* stats,
-                                            const float* gamma, const float* beta, int silu, const bf16* dy,
-                                            int lddy, float* xh, float* gdy, float* rsv) {
-  float f[8], d[8];
-  gn_load8(s, n, row, cg * 8, f);
-  load8(dy + ((long)n * s.hw + row) * lddy + cg * 8, d);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = cg * 8 + i, g = c / s.cpg;
-    const float mu = stats[((long)n * s.groups + g) * 2], rs = stats[((long)n * s.groups + g) * 2 + 1];
-    const float xhat = (f[i] - mu) * rs;
-    float dd = d[i];
-    if (silu) {
-      const float yv = (float)(bf16)(xhat * gamma[c] + beta[c]);
-      dd = (float)(bf16)(dd * silu_grad(yv));
-    }
-    xh[i] = xhat;
-    gdy[i] = dd * gamma[c];
-    rsv[i] = rs;
-  }
-}
-
 __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
                                     const bf16* dy, int lddy, float* part) {
   extern __shared__ float sh[];
@@ -189,12 +167,33 @@ __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* 
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (r0 < s.R) {
+    // per-thread channel coefficients, once (the row loop carries no divisions or table loads)
+    float mu[8], rsd[8], ga[8], be[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = cg * 8 + i, g = c / s.cpg;
+      mu[i] = stats[((long)n * s.groups + g) * 2];
+      rsd[i] = stats[((long)n * s.groups + g) * 2 + 1];
+      ga[i] = gamma[c];
+      be[i] = beta[c];
+    }
     const int rbeg = chunk * s.rows_per_chunk, rend = min(s.hw, rbeg + s.rows_per_chunk);
     for (int row = rbeg + r0; row < rend; row += s.R) {
-      float xh[8], gdy[8], rs[8];
-      gn_bwd_elem(s, n, row, cg, stats, gamma, beta, silu, dy, lddy, xh, gdy, rs);
+      float f[8], d[8];
+      gn_load8(s, n, row, cg * 8, f);
+      load8(dy + ((long)n * s.hw + row) * lddy + cg * 8, d);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { a[i] += gdy[i]; b[i] += gdy[i] * xh[i]; }
+      for (int i = 0; i < 8; ++i) {
+        const float xhat = (f[i] - mu[i]) * rsd[i];
+        float dd = d[i];
+        if (silu) {
+          const float yv = (float)(bf16)(xhat * ga[i] + be[i]);
+          dd = (float)(bf16)(dd * silu_grad(yv));
+        }
+        const float gd = dd * ga[i];
+        a[i] += gd;
+        b[i] += gd * xhat;
+      }
     }
   }
   gn_block_fold(s, a, b, sh, part + ((long)n * s.nchunk + chunk) * s.groups * 2);
