@@ -159,7 +159,8 @@ __global__ void gn_apply_kernel(GNShape s, const float* stats, const float* gamm
   }
 }
 
-// dy' = dy * silu'(y) (y = gn(x) rounded to bf16, dy' rounded to bf16), as autograd does on bf16
+// backward statistics: (sum g dy', sum g dy' xhat) per group, dy' = dy * silu'(y) with y = gn(x) rounded
+// to bf16 and dy' rounded to bf16, as autograd does on bf16
 __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
                                     const bf16* dy, int lddy, float* part) {
   extern __shared__ float sh[];
@@ -394,7 +395,7 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
     ga[i] = act ? gamma[ch + i] : 0.0f;
     be[i] = act ? beta[ch + i] : 0.0f;
   }
-  // dy' = dy * silu'(y) rounded as bf16 autograd does (gn_bwd_elem); returns g * dy' and xhat
+  // dy' = dy * silu'(y) rounded as bf16 autograd does (as gn_bwd_stats_kernel); returns g * dy' and xhat
   auto elem = [&](float f, float d, int i, float& xh) {
     xh = (f - mu) * rs;
     float dd = d;
