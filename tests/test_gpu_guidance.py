@@ -128,3 +128,66 @@ def test_per_input_dense_loss_grad(funcs):
     torch.cuda.synchronize()
     assert torch.allclose(lossv.cpu(), loss.detach(), rtol=1e-3, atol=1e-5)
     assert torch.allclose(grad2[:, 0].cpu(), sc.grad, rtol=2e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("ph,pw,rh,rw,h,w,nearest", [(48, 64, 48, 64, 48, 64, 0), (48, 64, 45, 60, 90, 120, 0),
+                                                    (48, 64, 45, 60, 90, 120, 1), (16, 24, 16, 24, 37, 50, 0)])
+def test_decode_row_sets(ph, pw, rh, rw, h, w, nearest):
+    """dc_tap_mask / dc_dilate_mask / dc_mask_count + dc_mask_rows against a torch restatement: the resize taps
+    of the sparse pixels (upsample_bilinear2d align_corners=False source indices, or nearest), 3x3 dilation
+    within each frame, sorted compaction with the pad repeating the last index."""
+    import torch.nn.functional as F
+    from depth_completion_amd import _lib
+    from depth_completion_amd.ops import Ctx
+    ctx = Ctx(dev)
+    n, npts = 2, 70
+    g = torch.Generator().manual_seed(7)
+    idx = torch.zeros(n, h * w, dtype=torch.int32)
+    ref = torch.zeros(n, ph, pw, dtype=torch.bool)
+    for i in range(n):
+        p = torch.randperm(h * w, generator=g)[:npts].sort().values
+        idx[i, :npts] = p.int()
+        for q in p.tolist():
+            y, x = divmod(q, w)
+            if nearest:
+                ys = [y if rh == h else min(int(y * (rh / h)), rh - 1)]
+                xs = [x if rw == w else min(int(x * (rw / w)), rw - 1)]
+            elif rh == h and rw == w:
+                ys, xs = [y], [x]
+            else:
+                sy = max((rh / h) * (y + 0.5) - 0.5, 0.0)
+                sx = max((rw / w) * (x + 0.5) - 0.5, 0.0)
+                y0, x0 = int(sy), int(sx)
+                ys = [y0, y0 + (1 if y0 < rh - 1 else 0)]
+                xs = [x0, x0 + (1 if x0 < rw - 1 else 0)]
+            for yy in ys:
+                for xx in xs:
+                    ref[i, yy, xx] = True
+    params = torch.zeros(n, 8)
+    params[:, 7] = 8.0 * nearest
+    cnt = torch.full((n,), npts, dtype=torch.int32)
+    idx_d, cnt_d, par_d = idx.to(dev), cnt.to(dev), params.to(dev)
+    total = n * ph * pw
+    m0 = torch.empty(total, dtype=torch.uint8, device=dev)
+    m1 = torch.empty(total, dtype=torch.uint8, device=dev)
+    _lib.call("dc_tap_mask", idx_d.data_ptr(), cnt_d.data_ptr(), par_d.data_ptr(), n, ph, pw, rh, rw, h, w,
+              m0.data_ptr(), ctx.stream)
+    _lib.call("dc_dilate_mask", m0.data_ptr(), n, ph, pw, m1.data_ptr(), ctx.stream)
+    torch.cuda.synchronize()
+    assert torch.equal(m0.view(n, ph, pw).bool().cpu(), ref)
+    dil = F.max_pool2d(ref.float()[:, None], 3, stride=1, padding=1)[:, 0] > 0
+    assert torch.equal(m1.view(n, ph, pw).bool().cpu(), dil)
+    ws = torch.empty(-(-_lib.load().dc_mask_rows_ws_bytes(total) // 4), dtype=torch.int32, device=dev)
+    cntr = torch.zeros(1, dtype=torch.int32, device=dev)
+    _lib.call("dc_mask_count", m1.data_ptr(), total, ws.data_ptr(), cntr.data_ptr(), ctx.stream)
+    c = int(cntr.item())
+    want = torch.nonzero(dil.flatten()).flatten().int()
+    assert c == want.numel()
+    pad = c + 37
+    rows = torch.full((pad,), -1, dtype=torch.int32, device=dev)
+    _lib.call("dc_mask_rows", m1.data_ptr(), total, ws.data_ptr(), cntr.data_ptr(), pad, rows.data_ptr(),
+              ctx.stream)
+    torch.cuda.synchronize()
+    rows = rows.cpu()
+    assert torch.equal(rows[:c], want)
+    assert bool((rows[c:] == want[-1]).all())
