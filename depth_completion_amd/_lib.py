@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -41,6 +41,7 @@ class ConvDesc(C.Structure):
 # name -> argtypes (all return int status unless listed in _RESTYPE)
 _SIGS = {
     "dc_abi_version": [],
+    "dc_build_id": [],
     "dc_conv_num_algos": [],
     "dc_conv_gemm": [C.POINTER(ConvDesc), vp],
     "dc_groupnorm_ws_bytes": [i32, i32, i32, i32],
@@ -69,7 +70,7 @@ _SIGS = {
     "dc_latent_update": [vp, vp, vp, vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp, i64,
                          vp],
     "dc_step_advance": [vp, i32, vp],
-    "dc_latent_init": [vp, vp, f32, i32, i32, vp, vp],
+    "dc_latent_init": [vp, i32, vp, f32, i32, i32, vp, vp],
     "dc_final_dense": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp],
     "dc_ddim_step": [vp, vp, i32, i32, vp, vp, vp],
     "dc_closed_form_affine": [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
@@ -94,8 +95,11 @@ _SIGS = {
     "dc_transpose": [vp, i32, i32, i32, vp, i32, vp],
     "dc_depth_metrics_ws_bytes": [],
     "dc_depth_metrics": [vp, vp, i64, f32, f32, vp, i32, vp, vp, vp],
+    "dc_ensemble_ws_bytes": [i32, i64],
+    "dc_ensemble_fit": [vp, i32, i32, i64, vp, vp, vp, vp, i64, vp],
 }
-_RESTYPE = {"dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64}
+_RESTYPE = {"dc_build_id": C.c_char_p, "dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64,
+             "dc_ensemble_ws_bytes": i64}
 
 STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}
 
@@ -126,8 +130,27 @@ def load():
         fn.restype = _RESTYPE.get(name, i32)
     if lib.dc_abi_version() != ABI_VERSION:
         raise DCError(f"libdcamd ABI {lib.dc_abi_version()} != expected {ABI_VERSION}; rebuild")
+    check_provenance(lib)
     _lib = lib
     return lib
+
+
+def build_id(lib=None) -> str:
+    return (lib or load()).dc_build_id().decode()
+
+
+def check_provenance(lib) -> None:
+    """Refuse a library whose build id differs from the hash of the sources in this tree (a stale or foreign
+    binary); DC_LIB (an explicit A/B library) skips the check, as does a tree shipped without sources."""
+    if os.environ.get("DC_LIB"):
+        return
+    from . import build as _build
+    if not all(f.exists() for f in _build.source_files()):
+        return
+    want, have = _build.source_hash(), lib.dc_build_id().decode()
+    if want != have:
+        raise DCError(f"{_LIB_PATH} was built from other sources (build id {have}, tree {want}): rebuild it with "
+                      "`python -m depth_completion_amd.build`")
 
 
 def exported_symbols() -> list[str]:

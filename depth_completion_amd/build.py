@@ -5,6 +5,7 @@ without a GPU, so this runs in the CPU container too.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -16,10 +17,24 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libdcamd.so"
 OBJ_DIR = PKG / "build_obj"
 SOURCES = ["conv_gemm.hip", "norms.hip", "attention.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
-           "rowsets.hip", "version.hip"]
+           "rowsets.hip", "ensemble.hip", "version.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DC_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def source_files() -> list[Path]:
+    """Every file libdcamd.so is compiled from (the build id hashes exactly these)."""
+    return [CSRC / s for s in SOURCES] + [CSRC / "common.h", PKG.parent / "include" / "dcamd.h"]
+
+
+def source_hash() -> str:
+    """sha256 (first 16 hex digits) over the library's sources: the build id compiled into libdcamd.so
+    (dc_build_id) and checked by _lib.load() against the tree it runs from."""
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()[:16]
 
 
 def _needs(obj: Path, deps: list[Path]) -> bool:
@@ -32,12 +47,18 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
 def build(verbose: bool = False, force: bool = False) -> Path:
     OBJ_DIR.mkdir(exist_ok=True)
     headers = [CSRC / "common.h", PKG.parent / "include" / "dcamd.h"]
+    bid = source_hash()
     jobs = []
     for src in SOURCES:
         s = CSRC / src
         o = OBJ_DIR / (src + ".o")
-        if force or _needs(o, [s, *headers]):
-            jobs.append([HIPCC, *FLAGS, "-c", str(s), "-o", str(o)])
+        extra = []
+        deps = [s, *headers]
+        if src == "version.hip":   # carries the build id: rebuilt whenever any source changes
+            extra = [f'-DDC_BUILD_ID="{bid}"']
+            deps = source_files()
+        if force or _needs(o, deps):
+            jobs.append([HIPCC, *FLAGS, *extra, "-c", str(s), "-o", str(o)])
 
     def run(cmd):
         if verbose:

@@ -561,13 +561,17 @@ __global__ void step_advance_kernel(int* step, int nsteps) {
 
 // initial depth latents (marigold_dc.py:677-704): noise [1][4][hw] (NCHW, repeated over frames),
 // optional warm start beta*noise + (1-beta)*prev (prev [nb][4][hw]) -> x8[...,4:8]
-__global__ void latent_init_kernel(const bf16* noise, const bf16* prev, float beta, int nb, int hw, bf16* x8) {
+// noise [noise_frames][4][hw]: one draw shared by every frame (noise_frames 1, marigold_dc.py:677-684), or
+// one per frame (noise_frames == nb: the per-seed draws of an ensemble batch)
+__global__ void latent_init_kernel(const bf16* noise, int noise_frames, const bf16* prev, float beta, int nb, int hw,
+                                   bf16* x8) {
   const long total = (long)nb * hw * 4;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
     const int p = (int)(i % hw);
     const int k = (int)((i / hw) % 4);
     const long n = i / ((long)hw * 4);
-    float v = (float)noise[(long)k * hw + p];
+    const long nf = noise_frames > 1 ? n : 0;
+    float v = (float)noise[(nf * 4 + k) * hw + p];
     if (prev) {
       const float a = (float)(bf16)(beta * v);
       const float b = (float)(bf16)((1.0f - beta) * (float)prev[i]);
@@ -1190,11 +1194,11 @@ extern "C" int dc_step_advance(int* step, int nsteps, void* stream) {
   return DC_OK;
 }
 
-extern "C" int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8,
-                              void* stream) {
-  if (!noise || !x8 || nb <= 0 || hw <= 0) return DC_ERR_ARG;
+extern "C" int dc_latent_init(const void* noise, int noise_frames, const void* prev, float beta, int nb, int hw,
+                              void* x8, void* stream) {
+  if (!noise || !x8 || nb <= 0 || hw <= 0 || (noise_frames != 1 && noise_frames != nb)) return DC_ERR_ARG;
   hipLaunchKernelGGL(latent_init_kernel, grid_for((long)nb * hw * 4), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16*)noise, (const bf16*)prev, beta, nb, hw, (bf16*)x8);
+                     (const bf16*)noise, noise_frames, (const bf16*)prev, beta, nb, hw, (bf16*)x8);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

@@ -228,11 +228,14 @@ class MarigoldDepthCompletionPipeline:
         gen = torch.Generator().manual_seed(seed)
         noise = torch.randn((1, 4, h, w), generator=gen, dtype=BF16) if init_noise is None else init_noise
         noise = noise.to(dev, BF16).contiguous()
+        # one draw for every frame, or one per frame (the per-seed draws of ensemble())
+        if noise.ndim != 4 or tuple(noise.shape[1:]) != (4, h, w) or noise.shape[0] not in (1, n):
+            raise ValueError(f"init_noise must be [1, 4, {h}, {w}] or [{n}, 4, {h}, {w}], got {tuple(noise.shape)}")
         prev = None
         if pred_latents_prev is not None:
             prev = pred_latents_prev.to(dev, BF16).contiguous()
-        _lib.call("dc_latent_init", noise.data_ptr(), ops.P(prev), float(beta), n, h * w, up.x8.data_ptr(),
-                  ctx.stream)
+        _lib.call("dc_latent_init", noise.data_ptr(), noise.shape[0], ops.P(prev), float(beta), n, h * w,
+                  up.x8.data_ptr(), ctx.stream)
 
         # ---- image latents (marigold_dc.py:687-698): preprocess + TAESD encoder into x8[..., 0:4]
         img8 = torch.empty(n * PH * PW, 8, dtype=BF16, device=dev)
@@ -362,6 +365,56 @@ class MarigoldDepthCompletionPipeline:
         self.last_loss = st["loss"]
         return dense, lat
 
+    # ------------------------------------------------------------------ seed ensemble (BASELINE C5)
+    DEFAULT_SEEDS = tuple(range(2024, 2034))
+
+    def ensemble(self, imgs, sparses, max_depth, seeds=DEFAULT_SEEDS, init_noise=None, resolution=768, **kw):
+        """Seed ensemble per frame (BASELINE.json config C5): every frame is sampled once per
+        seed -- the N x S samples run as ONE batched guided call, frame-major (frames never interact,
+        marigold_dc.py:877), each with the initial noise ``__call__`` draws for that seed (CPU
+        ``torch.Generator(seed)``, [1, 4, h, w]; or ``init_noise[k]`` for seed k) -- then the per-pixel mean
+        of the S dense maps is fitted to the sparse depth with compute_affine_params (marigold_dc.py:53-128)
+        on the device (dc_ensemble_fit).  ``kw`` are ``__call__``'s keyword arguments (seed excluded).
+
+        Returns (dense fp32 [N, 1, H, W] metres, affine fp32 [N, 2] (scale, shift), latents bf16
+        [N * S, 4, h, w] frame-major)."""
+        if "seed" in kw:
+            raise ValueError("ensemble() takes seeds=..., not seed=")
+        seeds = list(seeds)
+        S = len(seeds)
+        if S == 0:
+            raise ValueError("seeds must not be empty")
+        if imgs.ndim != 4 or sparses.ndim != 4 or imgs.shape[0] != sparses.shape[0]:
+            raise ValueError("Shape of image must be [N, C, H, W] and shape of sparse must be "
+                             f"[N, 1, H, W], but got image.shape: {imgs.shape} and sparse.shape: {sparses.shape}")
+        n, _, H, W = imgs.shape
+        h, w = self.latent_hw(H, W, resolution)
+        if init_noise is None:
+            init_noise = torch.cat([torch.randn((1, 4, h, w), generator=torch.Generator().manual_seed(int(sd)),
+                                                dtype=BF16) for sd in seeds])
+        if tuple(init_noise.shape) != (S, 4, h, w):
+            raise ValueError(f"init_noise must be [{S}, 4, {h}, {w}] (one draw per seed), got {tuple(init_noise.shape)}")
+        dev = self.device
+        noise = init_noise.to(dev, BF16).repeat(n, 1, 1, 1)                  # [n*S]: frame f, seed k -> k
+        imgs_r = imgs.to(dev).repeat_interleave(S, dim=0)
+        sp = sparses.to(dev, torch.float32).contiguous()
+        sp_r = sp.repeat_interleave(S, dim=0)
+        dense, lat = self(imgs_r, sp_r, max_depth, init_noise=noise, resolution=resolution, **kw)
+        out = torch.empty(n, 1, H, W, dtype=torch.float32, device=dev)
+        affine = torch.empty(n, 2, dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        nws = lib.dc_ensemble_ws_bytes(n, H * W)
+        ws = torch.empty(-(-nws // 8), dtype=torch.float64, device=dev)
+        _lib.call("dc_ensemble_fit", dense.data_ptr(), n, S, H * W, sp.data_ptr(), out.data_ptr(), affine.data_ptr(),
+                  ws.data_ptr(), nws, self.ctx.stream)
+        return out, affine, lat
+
+    @staticmethod
+    def latent_hw(H, W, resolution=768):
+        """Latent (h, w) of an H x W input at the processing resolution (padded preprocessing size / 8)."""
+        m = max(H, W)
+        return -(-(H * resolution // m) // 8), -(-(W * resolution // m) // 8)
+
     # sets S0..S5 of taesd.DecoderPlan.set_rows, each padded up to a bucket -- a multiple of
     # max(_ROW_PAD, next_pow2(count) / 4) rows -- so that frames with similar point counts share launch
     # shapes and replay the captured step graph instead of recapturing it (padding rows repeat the last
@@ -418,8 +471,8 @@ class MarigoldDepthCompletionPipeline:
     def _reset_state(self, st, n, noise, prev, beta):
         ctx = self.ctx
         up = st["unet"]
-        _lib.call("dc_latent_init", noise.data_ptr(), ops.P(prev), float(beta), n, up.h * up.w, up.x8.data_ptr(),
-                  ctx.stream)
+        _lib.call("dc_latent_init", noise.data_ptr(), noise.shape[0], ops.P(prev), float(beta), n, up.h * up.w,
+                  up.x8.data_ptr(), ctx.stream)
         for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"]):
             ops.memset(ctx, t)
         st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))

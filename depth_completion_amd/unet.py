@@ -33,7 +33,10 @@ class ResnetW:
         self.shortcut = None
         if pre + "conv_shortcut.weight" in sd:
             self.shortcut = Conv(sd[pre + "conv_shortcut.weight"], sd[pre + "conv_shortcut.bias"], dev)
-        self.temb_table = None  # [S][cout] bf16, per call
+        self.temb_table = None  # [S][cout] bf16: the current call's entry of temb_tables
+        # one table per step count, never freed: a captured step graph binds the table's address, and a
+        # call with another step count must not free the one an earlier graph replays against
+        self.temb_tables: dict = {}
 
 
 class TransformerW:
@@ -133,9 +136,10 @@ class UNetHIP:
         semb = torch.empty_like(emb)
         ops.silu(ctx, emb, semb)
         for r in self.resnets():
-            # tables keep their address across calls with the same step count (hipGraph replay)
-            if r.temb_table is None or r.temb_table.shape[0] != S:
-                r.temb_table = torch.empty(S, r.cout, dtype=BF16, device=self.device)
+            # one table per step count, kept for the UNet's lifetime (hipGraph replay binds its address)
+            if S not in r.temb_tables:
+                r.temb_tables[S] = torch.empty(S, r.cout, dtype=BF16, device=self.device)
+            r.temb_table = r.temb_tables[S]
             ops.linear(ctx, semb, r.temb.wf, S, r.cout, r.temb_table, bias=r.temb.bias)
 
     def plan(self, ctx: Ctx, nb: int, h: int, w: int) -> "UNetPlan":

@@ -19,6 +19,8 @@ extern "C" {
 #endif
 
 int dc_abi_version(void);
+/* sha256 prefix (16 hex digits) of the sources this library was built from (build provenance) */
+const char* dc_build_id(void);
 
 /* ---------------------------------------------------------------- matmul-shaped ops
  * Implicit-GEMM conv / linear on MFMA.  Replaces the cuDNN conv fwd/dgrad and cuBLAS GEMMs that
@@ -161,7 +163,11 @@ int dc_latent_update(void* x8, const void* v, const void* gdir, const void* gune
 /* ws (nb * ceil(hw / 256) floats; may be null): per-block partials of ||g||^2 for the two-launch form
  * (kld_mode 0 / 1); without it (or with the strict KL term) one block per frame does both passes */
 int dc_step_advance(int* step, int nsteps, void* stream);  /* saturates at nsteps-1 */
-int dc_latent_init(const void* noise, const void* prev, float beta, int nb, int hw, void* x8, void* stream);
+/* initial latents (marigold_dc.py:661, 677-704): x8[..., 4:8] <- noise, or beta * noise + (1 - beta) * prev;
+ * noise bf16 [noise_frames][4][hw] NCHW: noise_frames 1 = one draw shared by all nb frames (the reference's
+ * single generator draw), noise_frames nb = one draw per frame (the per-seed draws of a seed ensemble) */
+int dc_latent_init(const void* noise, int noise_frames, const void* prev, float beta, int nb, int hw, void* x8,
+                   void* stream);
 int dc_final_dense(const void* dec_out, int ldo, int nb, int ph, int pw, int rh, int rw, int h, int w,
                    const float* params, const float* affine, int mode, float* dense, void* stream);
 /* mode 0 learned affine (marigold_dc.py:323-331), 1 closed form (:332-336) */
@@ -250,6 +256,16 @@ int dc_transpose(const void* x, int ldx, int rows, int cols, void* y, int ldy, v
 long long dc_depth_metrics_ws_bytes(void);
 int dc_depth_metrics(const float* dense, const float* sparse, long long total, float min_depth, float max_depth,
                      const float* bins, int nbins, double* ws, double* res, void* stream);
+
+/* ---------------------------------------------------------------- seed ensemble (BASELINE C5)
+ * The S seeds of each frame run as S frames of one guided call (per-frame noise, dc_latent_init).
+ * dense fp32 [frames*seeds][hw] frame-major (frame f's seeds are rows f*seeds ..), guide fp32 [frames][hw]
+ * (metres, > 0 = valid).  out[f] = scale_f * mean_seeds(dense) + shift_f with (scale_f, shift_f) =
+ * compute_affine_params(mean, guide, guide > 0) (marigold_dc.py:53-128; fp64 sums, same centring);
+ * affine (optional) [frames][2] gets (scale, shift).  ws >= dc_ensemble_ws_bytes(frames, hw), 8-B aligned. */
+long long dc_ensemble_ws_bytes(int frames, long long hw);
+int dc_ensemble_fit(const float* dense, int frames, int seeds, long long hw, const float* guide, float* out,
+                    float* affine, void* ws, long long ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -374,3 +374,15 @@ class OracleMarigoldDC(MarigoldBase):
                                        closed_form=closed_form, interp_mode=interp_mode).clamp(0.0, 1.0)
             dense = d * (hi - lo) + lo
         return dense, out_lat
+
+
+# ------------------------------------------------- seed ensemble (BASELINE.json config C5)
+def ensemble(pipe, imgs, sparses, max_depth, noises, **kw):
+    """C5's per-frame seed ensemble: one reference call per seed (initial noise ``noises[k]`` [1, 4, h, w]),
+    the mean of the dense maps over the seeds (torch.stack(...).mean(0)), then compute_affine_params
+    (marigold_dc.py:53-128) of the mean against the sparse depth over sparses > 0, applied.
+    Returns (fitted dense [N, 1, H, W], scale [N], shift [N])."""
+    denses = [pipe(imgs, sparses, max_depth, init_noise=nz, **kw)[0].float() for nz in noises]
+    mean = torch.stack(denses).mean(0)
+    scale, shift = compute_affine_params(mean, sparses.float(), sparses > 0)
+    return mean * scale.view(-1, 1, 1, 1) + shift.view(-1, 1, 1, 1), scale, shift

@@ -1,0 +1,175 @@
+"""Parity of the HIP guided sampler at the BASELINE.json workloads themselves (GPU).
+
+* C2: one 768x576 frame, 500 points, the full Marigold v1-0 UNet, 50 guided steps, norm="const" -- the
+  headline config (latent 72x96: T = 6912 tokens at level 0, the tuned GEMM table, stream-K attention
+  backward, the sparse-aware decode), against the fp32 oracle (oracle/pipeline_ref.py on PyTorch-ROCm)
+  after the reference's closed-form fit (compute_affine_params, marigold_dc.py:53-128).  Bound: at most
+  2x the oracle's own bf16 execution's error (+1e-3) -- 50 chained bf16 Adam + DDIM steps amplify
+  rounding identically in both -- and below the absolute 2 % mean / 8 % p99 of the frame's depth range.
+* C3: the same frame inside a batch of 8 (batched MFMA path, M = 8 x 6912); frames never interact
+  (marigold_dc.py:877), so every frame of the batch equals its own single-frame run within the same
+  bf16 bound.
+* C1: a 384x384 image at processing resolution 768 (latent 96x96, T = 9216 -- a shape the tuned table
+  never saw), 100 points, 10 guided steps.
+* C5: the 10-seed ensemble (seeds 2024..2033) + affine fit at the 1600x900 shape, tiny UNet, against the
+  oracle's per-seed loop + mean + compute_affine_params; and dc_ensemble_fit alone against the
+  reference's compute_affine_params on identical inputs.
+Every test prints the measured errors.
+"""
+import pytest
+import torch
+
+from oracle import pipeline_ref as P
+from oracle.diffusers_ref import UNetConfig, tiny_unet_config
+from test_gpu_pipeline import build, fitted_error, synth_inputs
+
+pytestmark = pytest.mark.gpu
+dev = torch.device("cuda:0")
+
+
+def _noise(seed, eh, ew):
+    return torch.randn((1, 4, eh, ew), generator=torch.Generator().manual_seed(seed), dtype=torch.bfloat16)
+
+
+def _lat_err(a, ref):
+    return float((a.float().cpu() - ref.float().cpu()).norm() / ref.float().cpu().norm())
+
+
+@pytest.fixture(scope="module")
+def full_c2():
+    """fp32 / bf16 oracle and the HIP pipeline on the full UNet, C2 frame 0 (shared by the C2 / C3 tests)."""
+    from depth_completion_amd.config import MARIGOLD_V1
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    imgs, sparses = synth_inputs(8, 576, 768, 500, seed=41)
+    kw = dict(norm="const", steps=50, resolution=768, init_noise=_noise(2024, 72, 96))
+    o32, usd, vsd, emb = build(UNetConfig(), MARIGOLD_V1, torch.float32, dev)
+    d32, l32 = o32(imgs[:1].to(dev), sparses[:1].to(dev), 120.0, **kw)
+    del o32
+    o16, *_ = build(UNetConfig(), MARIGOLD_V1, torch.bfloat16, dev)
+    d16, l16 = o16(imgs[:1].to(dev), sparses[:1].to(dev), 120.0, **kw)
+    del o16
+    torch.cuda.empty_cache()
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=MARIGOLD_V1, device=dev)
+    return dict(imgs=imgs, sparses=sparses, kw=kw, d32=d32.cpu(), l32=l32.cpu(), d16=d16.cpu(), l16=l16.cpu(),
+                pipe=pipe)
+
+
+def test_c2_full_unet_50_steps(full_c2):
+    f = full_c2
+    dh, lh = f["pipe"](f["imgs"][:1].to(dev), f["sparses"][:1].to(dev), 120.0, **f["kw"])
+    torch.cuda.synchronize()
+    assert dh.shape == (1, 1, 576, 768) and lh.shape == (1, 4, 72, 96) and torch.isfinite(dh).all()
+    sp = f["sparses"][:1]
+    mean_h, p99_h = fitted_error(dh, f["d32"], sp)
+    mean_b, p99_b = fitted_error(f["d16"], f["d32"], sp)
+    lat_h, lat_b = _lat_err(lh, f["l32"]), _lat_err(f["l16"], f["l32"])
+    print(f"\nC2 (full UNet, 768x576, 500 pts, 50 steps): HIP fitted |d| mean {mean_h:.5f} p99 {p99_h:.5f} "
+          f"latent {lat_h:.4f} | oracle-bf16 mean {mean_b:.5f} p99 {p99_b:.5f} latent {lat_b:.4f}")
+    assert mean_h <= 2 * mean_b + 1e-3 and p99_h <= 2 * p99_b + 1e-3
+    assert mean_h <= 0.02 and p99_h <= 0.08
+    assert lat_h <= 2 * lat_b + 2e-3
+
+
+def test_c3_batch8_frames_equal_single_runs(full_c2):
+    """Batch 8 through the batched path: each frame vs its own batch-1 run (same initial noise, which the
+    reference shares across the batch, marigold_dc.py:677-684); bound = the bf16 oracle's C2 error."""
+    f = full_c2
+    pipe = f["pipe"]
+    imgs, sparses = f["imgs"], f["sparses"]
+    db, lb = pipe(imgs.to(dev), sparses.to(dev), 120.0, **f["kw"])
+    torch.cuda.synchronize()
+    assert db.shape == (8, 1, 576, 768) and lb.shape == (8, 4, 72, 96) and torch.isfinite(db).all()
+    db, lb = db.cpu(), lb.cpu()
+    mean_b, p99_b = fitted_error(f["d16"], f["d32"], sparses[:1])
+    lat_b = _lat_err(f["l16"], f["l32"])
+    worst = (0.0, 0.0, 0.0)
+    for i in (0, 3, 7):
+        ds, ls = pipe(imgs[i:i + 1].to(dev), sparses[i:i + 1].to(dev), 120.0, **f["kw"])
+        m, p99 = fitted_error(db[i:i + 1], ds.cpu(), sparses[i:i + 1])
+        la = _lat_err(lb[i:i + 1], ls)
+        print(f"\nC3 frame {i}: batch-8 vs single fitted |d| mean {m:.5f} p99 {p99:.5f} latent {la:.4f}")
+        worst = tuple(max(a, b) for a, b in zip(worst, (m, p99, la)))
+        assert m <= 2 * mean_b + 1e-3 and p99 <= 2 * p99_b + 1e-3 and la <= 2 * lat_b + 2e-3
+    print(f"C3 worst over frames 0/3/7: mean {worst[0]:.5f} p99 {worst[1]:.5f} latent {worst[2]:.4f} "
+          f"(bound from the bf16 oracle: mean {2 * mean_b + 1e-3:.5f} p99 {2 * p99_b + 1e-3:.5f})")
+
+
+def test_c1_384_at_768_10_steps():
+    from depth_completion_amd.config import MARIGOLD_V1
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    imgs, sparses = synth_inputs(1, 384, 384, 100, seed=0)
+    kw = dict(norm="const", steps=10, resolution=768, init_noise=_noise(2024, 96, 96))
+    o32, usd, vsd, emb = build(UNetConfig(), MARIGOLD_V1, torch.float32, dev)
+    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **kw)
+    del o32
+    o16, *_ = build(UNetConfig(), MARIGOLD_V1, torch.bfloat16, dev)
+    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **kw)
+    del o16
+    torch.cuda.empty_cache()
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=MARIGOLD_V1, device=dev)
+    dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **kw)
+    torch.cuda.synchronize()
+    assert dh.shape == (1, 1, 384, 384) and lh.shape == (1, 4, 96, 96) and torch.isfinite(dh).all()
+    mean_h, p99_h = fitted_error(dh, d32, sparses)
+    mean_b, p99_b = fitted_error(d16, d32, sparses)
+    lat_h, lat_b = _lat_err(lh, l32), _lat_err(l16, l32)
+    print(f"\nC1 (384x384 @ 768, latent 96x96, 10 steps): HIP fitted |d| mean {mean_h:.5f} p99 {p99_h:.5f} "
+          f"latent {lat_h:.4f} | oracle-bf16 mean {mean_b:.5f} p99 {p99_b:.5f} latent {lat_b:.4f}")
+    assert mean_h <= 2 * mean_b + 1e-3 and p99_h <= 2 * p99_b + 1e-3
+    assert mean_h <= 0.02 and p99_h <= 0.08
+    assert lat_h <= 2 * lat_b + 2e-3
+
+
+def test_ensemble_fit_kernel_matches_reference_fit():
+    """dc_ensemble_fit on identical inputs: mean over seeds, then compute_affine_params (fp64 sums on the
+    device; the reference's fp32 torch sums differ by rounding only)."""
+    from depth_completion_amd import _lib
+    g = torch.Generator().manual_seed(3)
+    n, S, H, W = 3, 10, 90, 160
+    dense = torch.rand(n * S, 1, H, W, generator=g) * 50 + 5
+    sp = torch.where(torch.rand(n, 1, H, W, generator=g) < 0.02, torch.rand(n, 1, H, W, generator=g) * 80 + 2,
+                     torch.zeros(()))
+    mean = dense.view(n, S, 1, H, W).double().mean(1)
+    sc, sh = P.compute_affine_params(mean, sp.double(), sp > 0)
+    ref = mean * sc.view(-1, 1, 1, 1) + sh.view(-1, 1, 1, 1)
+    lib = _lib.load()
+    nws = lib.dc_ensemble_ws_bytes(n, H * W)
+    ws = torch.empty(-(-nws // 8), dtype=torch.float64, device=dev)
+    out = torch.empty(n, 1, H, W, device=dev)
+    aff = torch.empty(n, 2, device=dev)
+    dd, spd = dense.to(dev), sp.to(dev)
+    _lib.call("dc_ensemble_fit", dd.data_ptr(), n, S, H * W, spd.data_ptr(), out.data_ptr(), aff.data_ptr(),
+              ws.data_ptr(), nws, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(aff[:, 0].double().cpu(), sc, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(aff[:, 1].double().cpu(), sh, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=1e-5, atol=1e-4)
+
+
+def test_c5_ensemble_10_seeds():
+    """C5 shape (1600x900 at resolution 768: latent 54x96, 3000 points) with the 10-seed ensemble, tiny UNet,
+    3 guided steps: HIP ensemble() (one batched call of 10 seeds) vs the oracle's per-seed loop."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    h, w = 900, 1600
+    imgs, sparses = synth_inputs(1, h, w, 3000, seed=50)
+    seeds = list(range(2024, 2034))
+    noises = [_noise(s, 54, 96) for s in seeds]
+    kw = dict(norm="const", steps=3, resolution=768)
+    cfg_o = tiny_unet_config()
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
+    r32, *_ = P.ensemble(o32, imgs.to(dev), sparses.to(dev), 120.0, noises, **kw)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
+    r16, *_ = P.ensemble(o16, imgs.to(dev), sparses.to(dev), 120.0, noises, **kw)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    dh, aff, lat = pipe.ensemble(imgs.to(dev), sparses.to(dev), 120.0, seeds=seeds, **kw)
+    torch.cuda.synchronize()
+    assert dh.shape == (1, 1, h, w) and aff.shape == (1, 2) and lat.shape == (10, 4, 54, 96)
+    assert torch.isfinite(dh).all()
+    rng = float(r32.max() - r32.min())
+    err_h = float((dh.cpu() - r32.cpu()).abs().mean()) / rng
+    err_b = float((r16.cpu() - r32.cpu()).abs().mean()) / rng
+    print(f"\nC5 10-seed ensemble (tiny UNet, 3 steps): HIP |d| {err_h:.5f} of range | oracle-bf16 {err_b:.5f}")
+    assert err_h <= 2 * err_b + 2e-3
+    # the seeds really differ (else the ensemble would be one sample ten times)
+    assert float((lat[0].float() - lat[1].float()).abs().mean()) > 1e-2

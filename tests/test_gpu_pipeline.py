@@ -431,3 +431,59 @@ def test_baseline_config_shapes(h, w, npts, density):
     print(f"\n{w}x{h}: HIP |d| {err_h:.5f} p99 {p99_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} "
           f"latent {lat_b:.4f}")
     assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
+
+
+def test_graph_cache_step_counts_aba():
+    """Plan A (2 frames, 6 steps), plan B (1 frame, 3 steps), plan A again: the second plan-A call replays
+    the graph captured in the first, against the time-embedding tables of its step count (kept per step
+    count, never freed), and equals a fresh pipeline's call bitwise (plan B's call reallocated
+    the tables and plan A's graph replayed the freed address)."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    cfg_o = tiny_unet_config()
+    unet = UNet2DConditionModel(cfg_o)
+    usd = synthetic_state_dict(unet, 11)
+    vsd = synthetic_taesd_state_dict(AutoencoderTiny(), 12)
+    emb = synthetic_text_embedding(13, cfg_o.cross_attention_dim)
+    imgs, sparses = synth_inputs(2, 48, 64, 60, seed=8)
+    a = dict(norm="const", steps=6, resolution=64)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    pipe(imgs.to(dev), sparses.to(dev), 120.0, **a)
+    g_a = pipe._plans[(2, 6, 8)]["graph"]
+    pipe(imgs[:1].to(dev), sparses[:1].to(dev), 120.0, **dict(a, steps=3))
+    torch.cuda.empty_cache()
+    junk = torch.full((1 << 22,), 7.0, device=dev)   # recycle freed blocks with garbage
+    d1, l1 = pipe(imgs.to(dev), sparses.to(dev), 120.0, **a)
+    assert pipe._plans[(2, 6, 8)]["graph"] is g_a   # replayed, not recaptured
+    fresh = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    d2, l2 = fresh(imgs.to(dev), sparses.to(dev), 120.0, **a)
+    torch.cuda.synchronize()
+    del junk
+    assert torch.equal(d1, d2) and torch.equal(l1, l2)
+
+
+def test_graph_replay_new_frames_same_bucket():
+    """Frame set A, then frame set B (other sparse points, same count, same row bucket) on one pipeline at
+    resolution 256 with the sparse-aware decode: B's call replays A's captured step graph with the tables and
+    decode row lists refreshed in place, and equals a fresh pipeline's run on B bitwise."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    cfg_o = tiny_unet_config()
+    usd = synthetic_state_dict(UNet2DConditionModel(cfg_o), 11)
+    vsd = synthetic_taesd_state_dict(AutoencoderTiny(), 12)
+    emb = synthetic_text_embedding(13, cfg_o.cross_attention_dim)
+    ia, sa = synth_inputs(2, 192, 256, 40, seed=60)
+    ib, sb = synth_inputs(2, 192, 256, 40, seed=61)
+    assert not torch.equal(sa, sb)
+    kw = dict(norm="const", steps=4, resolution=256)
+    pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    pipe(ia.to(dev), sa.to(dev), 120.0, **kw)
+    st = pipe._plans[(2, 24, 32)]
+    g_a, key_a = st["graph"], st["graph_key"]
+    assert key_a[-1] != ()                       # the sparse-aware decode row lists are in use
+    db, lb = pipe(ib.to(dev), sb.to(dev), 120.0, **kw)
+    assert st["graph"] is g_a and st["graph_key"] == key_a   # replayed, not recaptured
+    fresh = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+    df, lf = fresh(ib.to(dev), sb.to(dev), 120.0, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(db, df) and torch.equal(lb, lf)
