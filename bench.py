@@ -44,6 +44,11 @@ PEAK_HBM_GBS = 8000.0
 METRIC = "dense-depth frames/sec at 768x576, 50 guided steps; 1 & 8 MI355X"
 
 
+def log(msg: str) -> None:
+    """progress on stderr (a long run keeps writing; the JSON line alone goes to stdout)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def synth_frame(h, w, n_points, seed, pattern="uniform"):
     """Seeded RGB (smooth gradient + noise) + 8-bit quantised sparse depth.
     pattern "beams": 64 scan rows evenly spaced over the lower 60 % of the image, each pixel kept with
@@ -201,6 +206,7 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
         t0 = time.perf_counter()
         pipe(img[None], sp[None], 120.0, norm="const", steps=s, resolution=768)
         times[s] = time.perf_counter() - t0
+        log(f"cpu baseline: {s}-step oracle call {times[s]:.1f} s on {threads} threads")
     t_step = max(times[2] - times[1], 1e-3)
     t_fixed = max(times[1] - t_step, 0.0)
     t_frame = (t_fixed + steps * t_step) * seeds
@@ -336,15 +342,18 @@ def run_worker(args) -> None:
         if not dry:
             torch.cuda.synchronize(dev)
 
+    log(f"rank {rank}/{world}: pipeline ready, {args.warmup} warm-up + {args.steps} timed calls")
     for c in range(args.warmup):
         run(*frame_sets[c])
     sync()
+    log(f"rank {rank}: warm-up done")
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for c in range(args.warmup, calls):
         dense, _ = run(*frame_sets[c])
     sync()
+    log(f"rank {rank}: timed calls done ({time.perf_counter() - t0:.2f} s)")
     if world > 1:
         dist.barrier()
     mine = time.perf_counter() - t0
@@ -408,6 +417,7 @@ def run_worker(args) -> None:
         line["roofline"] = roofline
         line["launches"] = {"kernel_nodes_per_guided_step": nodes.get("kernel"), "graph_nodes": nodes}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not dry:
+        log("cpu baseline (oracle on the host cores)")
         line["cpu_baseline"] = cpu_baseline(H, W, args.points, args.denoise_steps, S, args.pattern)
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -1262,9 +1262,32 @@ extern "C" int dc_affine_step(int nb, const float* grad2, int it, float lr, int 
   return DC_OK;
 }
 
+// byte fill by a kernel (16-B vector stores, byte-granular head / tail), not hipMemsetAsync: replayed from a
+// hipGraph in a later call, the memset node that hipMemsetAsync captures did not clear the guided step's dA
+// gradient map (the replay kept the previous call's values, tools/diag_batch.py DIAG=state / sync; with this
+// kernel every replay equals the eager step bitwise), so every fill of the library is a kernel node
+__global__ void fill_bytes_kernel(unsigned char* p, unsigned char v, long long head, long long nvec, long long bytes) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned w = 0x01010101u * v;
+  const uint4 q = make_uint4(w, w, w, w);
+  uint4* pv = reinterpret_cast<uint4*>(p + head);
+  for (long long i = t0; i < nvec; i += stride) pv[i] = q;
+  for (long long i = t0; i < head; i += stride) p[i] = v;
+  for (long long i = head + nvec * 16 + t0; i < bytes; i += stride) p[i] = v;
+}
+
 extern "C" int dc_memset_async(void* ptr, int value, long long bytes, void* stream) {
   if (!ptr || bytes < 0) return DC_ERR_ARG;
-  if (hipMemsetAsync(ptr, value, (size_t)bytes, (hipStream_t)stream) != hipSuccess) return DC_ERR_LAUNCH;
+  if (bytes == 0) return DC_OK;
+  unsigned char* p = (unsigned char*)ptr;
+  long long head = (16 - ((uintptr_t)p & 15)) & 15;
+  if (head > bytes) head = bytes;
+  const long long nvec = (bytes - head) / 16;
+  const long long blocks = std::min<long long>(4096, std::max<long long>(1, (nvec + 255) / 256));
+  hipLaunchKernelGGL(fill_bytes_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p,
+                     (unsigned char)value, head, nvec, bytes);
+  DC_CHECK_LAUNCH();
   return DC_OK;
 }
 

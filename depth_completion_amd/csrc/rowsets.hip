@@ -148,7 +148,7 @@ extern "C" int dc_tap_mask(const int* idx, const int* cnt, const float* params, 
                            int rw, int h, int w, unsigned char* mask, void* stream) {
   if (!idx || !cnt || !params || !mask || nb <= 0 || rh > ph || rw > pw || h <= 0 || w <= 0) return DC_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(mask, 0, (size_t)nb * ph * pw, st) != hipSuccess) return DC_ERR_LAUNCH;
+  if (dc_memset_async(mask, 0, (long long)nb * ph * pw, stream) != DC_OK) return DC_ERR_LAUNCH;
   const long HW = (long)h * w;
   const dim3 g((unsigned)min((HW + 255) / 256, 1024L), nb);
   hipLaunchKernelGGL(tap_mask_kernel, g, dim3(256), 0, st, idx, cnt, params, ph, pw, rh, rw, h, w, mask);

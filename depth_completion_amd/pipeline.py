@@ -309,7 +309,11 @@ class MarigoldDepthCompletionPipeline:
             gkey = (guided, guided and cf, opt_code, kld_code, float(kld_weight), steps, H, W, RH, RW, lr_latent,
                     lr_scaling, loss_flags if full_loss else 0, row_counts)
             if g is None or st["graph_key"] != gkey:
-                # tables are rebuilt per call at new addresses: capture against this call's buffers
+                # (re)capture against this call's tables: they become the graph's tables before the warm-up and
+                # the capture read them through _tables(), and the previous graph is dropped first, as it binds
+                # the tables being replaced
+                st["graph"], st["graph_key"] = None, None
+                st["graph_tables"] = (coef, adam, idx, gval, cnt, params, gmap, img_u8)
                 g = torch.cuda.CUDAGraph()
                 torch.cuda.synchronize(dev)
                 s = torch.cuda.Stream(dev)
@@ -323,7 +327,6 @@ class MarigoldDepthCompletionPipeline:
                 with torch.cuda.graph(g):
                     step_fn(st)
                 st["graph"], st["graph_key"] = g, gkey
-                st["graph_tables"] = (coef, adam, idx, gval, cnt, params, gmap, img_u8)
             else:
                 # replay reads the captured table addresses: refresh their contents in place
                 old = st["graph_tables"]

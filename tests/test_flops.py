@@ -13,7 +13,8 @@ def test_survey_table(h, w, steps, seeds, ufwd, udgrad, dec, enc, frame):
     f = frame_flops(h, w, steps, seeds)
     for key, want in (("unet_fwd", ufwd), ("unet_dgrad", udgrad), ("taesd_dec", dec), ("taesd_enc", enc),
                       ("per_frame", frame)):
-        assert abs(f[key] / 1e12 - want) / want < 2e-3, (key, f[key] / 1e12, want)
+        # the table is rounded to 3 decimals: allow half a unit of its last digit
+        assert abs(f[key] / 1e12 - want) <= 5e-4 + 1e-3 * want, (key, f[key] / 1e12, want)
 
 
 def test_ensemble_scales_with_seeds():

@@ -546,3 +546,26 @@ def test_geglu_epilogues(ctx, algo, nsplit):
     (hh * F.gelu(gq)).backward(dgg)
     ref = torch.cat([hh.grad, gq.grad], 1)[:, perm]
     assert rel(df.float(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("nbytes,offset", [(1 << 10, 0), (1769472, 0), (5 << 20, 4), (3 * (1 << 20) + 7, 3)])
+def test_memset_in_graph_replays(nbytes, offset):
+    """dc_memset_async captured in a hipGraph clears its whole range on every replay, after the buffer has been
+    dirtied between replays (the guided step clears its dA map this way), and leaves the bytes around it."""
+    from depth_completion_amd import _lib
+    buf = torch.full((nbytes + 64,), 0xAB, dtype=torch.uint8, device=dev)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        _lib.call("dc_memset_async", buf.data_ptr() + offset, 0, nbytes, s.cuda_stream)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        _lib.call("dc_memset_async", buf.data_ptr() + offset, 0, nbytes, torch.cuda.current_stream().cuda_stream)
+    for val in (0x11, 0xFF, 0x5A):
+        buf.fill_(val)
+        g.replay()
+        torch.cuda.synchronize()
+        b = buf.cpu()
+        assert int(b[offset:offset + nbytes].count_nonzero()) == 0
+        assert bool((b[:offset] == val).all()) and bool((b[offset + nbytes:] == val).all())
