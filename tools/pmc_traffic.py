@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--regex", default="conv_gemm")
     ap.add_argument("--latent-shape", default="1,72,96", help="frames,h,w of the profiled step (C2 default)")
     ap.add_argument("--source", default="")
+    ap.add_argument("--mfma", default=None, help="counter_collection.csv of the SQ_VALU_MFMA_BUSY_CYCLES / "
+                                                 "GRBM_GUI_ACTIVE pass")
     a = ap.parse_args()
     fv, _ = per_dispatch(a.fetch, "FETCH_SIZE", a.regex)
     wv, _ = per_dispatch(a.write, "WRITE_SIZE", a.regex)
@@ -44,6 +46,15 @@ def main():
            "traffic_bytes_per_launch": fetch_b + write_b,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE as is; KiB -> bytes",
            "latent_shape": [int(v) for v in a.latent_shape.split(",")], "source": a.source}
+    if a.mfma:
+        # MFMA utilisation: SQ_VALU_MFMA_BUSY_CYCLES (matrix-pipe busy cycles summed over the SIMDs; 16 per
+        # v_mfma_f32_16x16x32_bf16) / (GRBM_GUI_ACTIVE / 8 XCDs = GPU cycles of the dispatch x 1024 SIMDs),
+        # summed over every conv_gemm dispatch of the pass
+        busy, _ = per_dispatch(a.mfma, "SQ_VALU_MFMA_BUSY_CYCLES", a.regex)
+        gui, _ = per_dispatch(a.mfma, "GRBM_GUI_ACTIVE", a.regex)
+        res["mfma_util"] = round(sum(busy.values()) / (sum(gui.values()) / 8.0 * 1024.0), 4)
+        res["mfma_util_def"] = ("sum SQ_VALU_MFMA_BUSY_CYCLES / (sum GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) over the "
+                                "conv_gemm dispatches of the pass")
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
