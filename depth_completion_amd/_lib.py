@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -98,7 +98,23 @@ _SIGS = {
     "dc_ensemble_ws_bytes": [i32, i64],
     "dc_ensemble_fit": [vp, i32, i32, i64, vp, vp, vp, vp, i64, vp],
 }
-_RESTYPE = {"dc_build_id": C.c_char_p, "dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64,
+_SIGS.update({
+    "dc_schedule_tables": [i32, C.c_double, C.c_double, i32, vp, vp, vp],
+    "dc_timestep_embedding": [vp, i32, i32, vp],
+    "dc_fold_cross_attention": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+    "dc_sample_params_default": [vp],
+    "dc_latent_hw": [i32, i32, i32, vp, vp],
+    "dc_create": [vp, i32],
+    "dc_destroy": [vp],
+    "dc_session_error": [vp],
+    "dc_load_weights": [vp, C.c_char_p, C.c_char_p],
+    "dc_encode": [vp, vp, i32, i32, i32, i32, vp, vp],
+    "dc_guided_sample": [vp, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp],
+    "dc_decode_dense": [vp, vp, vp, vp, i32, i32, i32, vp, vp, vp],
+    "dc_complete": [vp, vp, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp],
+})
+_RESTYPE = {"dc_session_error": C.c_char_p, "dc_sample_params_default": None,
+            "dc_build_id": C.c_char_p, "dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64,
              "dc_ensemble_ws_bytes": i64}
 
 STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}

@@ -1,0 +1,142 @@
+// Host-side (CPU) helpers shared by both hosts of the sampler -- the Python pipeline (pipeline.py, unet.py,
+// weights.py call them through ctypes) and the native session (session.cpp) -- so that the per-call tables
+// and load-time constants they feed to the kernels are the same bits on either host.
+//   dc_schedule_tables       DDIMScheduler (scaled_linear 0.00085..0.012, v_prediction, set_alpha_to_one=False,
+//                            timestep_spacing="trailing"; marigold_dc.py:800, 814, 823-826, 902-904, predict.py:491-494)
+//                            reduced to per-step scalars, and torch.optim.Adam's bias corrections (:783, 897)
+//   dc_timestep_embedding    diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), fp32
+//   dc_fold_cross_attention  attn2 with the constant 2-token empty-prompt context folded to (U, D, c0)
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/dcamd.h"
+
+namespace {
+inline float round_bf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return f;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  u &= 0xffff0000u;
+  float r;
+  memcpy(&r, &u, 4);
+  return r;
+}
+}  // namespace
+
+extern "C" int dc_schedule_tables(int steps, double lr_latent, double lr_scaling, int opt, long long* timesteps,
+                                  float* coef, float* adam) {
+  constexpr int T = 1000;
+  if (steps <= 0 || steps > T || opt < 0 || opt > 2) return 1;
+  // betas = linspace(sqrt(0.00085), sqrt(0.012), T, fp32) ** 2; alphas_cumprod = cumprod(1 - betas)
+  // (torch's linspace: start + step * i below the midpoint, end - step * (T - 1 - i) above; cumprod
+  // accumulates in double and stores fp32)
+  const float start = (float)std::sqrt(0.00085), end = (float)std::sqrt(0.012);
+  const float step = (end - start) / (float)(T - 1);
+  std::vector<float> ac(T);
+  double acc = 1.0;
+  for (int i = 0; i < T; ++i) {
+    volatile float prod = i < T / 2 ? step * (float)i : step * (float)(T - 1 - i);  // no fma contraction
+    const float lin = i < T / 2 ? start + prod : end - prod;
+    volatile float beta = lin * lin;
+    acc *= (double)(1.0f - beta);
+    ac[i] = (float)acc;
+  }
+  // trailing timesteps: round(arange(T, 0, -T / steps)) - 1 (numpy: start + i * delta, round half to even)
+  const double ratio = (double)T / steps;
+  const double delta = ((double)T + (-ratio)) - (double)T;
+  for (int s = 0; s < steps; ++s) {
+    const double v = (double)T + s * delta;
+    const long long t = (long long)std::nearbyint(v) - 1;
+    if (t < 0 || t >= T) return 1;
+    timesteps[s] = t;
+    const float a = ac[t];
+    const long long prev = t - T / steps;
+    const float ap = prev >= 0 ? ac[prev] : ac[0];
+    const float b = 1.0f - a;
+    coef[4 * s + 0] = std::sqrt(a);
+    coef[4 * s + 1] = std::sqrt(b);
+    coef[4 * s + 2] = std::sqrt(ap);
+    coef[4 * s + 3] = std::sqrt(1.0f - ap);
+    if (opt == 0) {
+      // Adam: Python doubles lr / (1 - beta1^k), (1 - beta2^k) ** 0.5, cast to fp32 (foreach kernels)
+      const int k = s + 1;
+      const double bc1 = 1.0 - std::pow(0.9, k), bc2 = 1.0 - std::pow(0.999, k);
+      adam[4 * s + 0] = (float)(lr_latent / bc1);
+      adam[4 * s + 1] = (float)std::pow(bc2, 0.5);
+      adam[4 * s + 2] = (float)(lr_scaling / bc1);
+      adam[4 * s + 3] = 0.0f;
+    } else {
+      adam[4 * s + 0] = (float)lr_latent;
+      adam[4 * s + 1] = 0.0f;
+      adam[4 * s + 2] = (float)lr_scaling;
+      adam[4 * s + 3] = 0.0f;
+    }
+  }
+  return 0;
+}
+
+extern "C" int dc_timestep_embedding(const long long* timesteps, int n, int dim, float* out) {
+  if (n <= 0 || dim <= 1 || (dim & 1) || !timesteps || !out) return 1;
+  const int half = dim / 2;
+  const float nlog = (float)(-std::log(10000.0));
+  std::vector<float> freq(half);
+  for (int i = 0; i < half; ++i) {
+    volatile float e = nlog * (float)i;
+    freq[i] = std::exp(e / (float)half);
+  }
+  for (int r = 0; r < n; ++r) {
+    const float t = (float)timesteps[r];
+    for (int i = 0; i < half; ++i) {
+      const float e = t * freq[i];
+      out[(long)r * dim + i] = std::cos(e);          // flip_sin_to_cos: [cos | sin]
+      out[(long)r * dim + half + i] = std::sin(e);
+    }
+  }
+  return 0;
+}
+
+extern "C" int dc_fold_cross_attention(const float* wq, const float* wk, const float* wv, const float* wo,
+                                       const float* bo, const float* ctx, int ntok, int inner, int c, int cross,
+                                       int cout, int heads, float* U, float* D, float* c0) {
+  // softmax over the 2 context tokens: p0 = sigmoid(q . (k0 - k1) / sqrt(hd)); out = v1 + p0 (v0 - v1) per head:
+  //   U_h = Wq_h^T (k0_h - k1_h) / sqrt(hd),  D_h = Wo_h (v0_h - v1_h),  c0 = Wo v1 + bo
+  // in double from bf16-rounded weights; k, v rounded to bf16 as the reference's to_k / to_v produce them
+  if (ntok != 2 || heads <= 0 || inner % heads || !wq || !wk || !wv || !wo || !bo || !ctx) return 1;
+  const int hd = inner / heads;
+  std::vector<double> k(2 * (size_t)inner), v(2 * (size_t)inner);
+  for (int t = 0; t < 2; ++t)
+    for (int j = 0; j < inner; ++j) {
+      double sk = 0.0, sv = 0.0;
+      for (int i = 0; i < cross; ++i) {
+        const double ci = round_bf16(ctx[(size_t)t * cross + i]);
+        sk += ci * round_bf16(wk[(size_t)j * cross + i]);
+        sv += ci * round_bf16(wv[(size_t)j * cross + i]);
+      }
+      k[(size_t)t * inner + j] = round_bf16((float)sk);
+      v[(size_t)t * inner + j] = round_bf16((float)sv);
+    }
+  const double scale = 1.0 / std::sqrt((double)hd);
+  for (int h = 0; h < heads; ++h) {
+    for (int col = 0; col < c; ++col) {
+      double s = 0.0;
+      for (int j = h * hd; j < (h + 1) * hd; ++j)
+        s += (double)round_bf16(wq[(size_t)j * c + col]) * (k[j] - k[(size_t)inner + j]);
+      U[(size_t)h * c + col] = (float)(s * scale);
+    }
+    for (int o = 0; o < cout; ++o) {
+      double s = 0.0;
+      for (int j = h * hd; j < (h + 1) * hd; ++j)
+        s += (double)round_bf16(wo[(size_t)o * inner + j]) * (v[j] - v[(size_t)inner + j]);
+      D[(size_t)h * cout + o] = (float)s;
+    }
+  }
+  for (int o = 0; o < cout; ++o) {
+    double s = 0.0;
+    for (int j = 0; j < inner; ++j) s += (double)round_bf16(wo[(size_t)o * inner + j]) * v[(size_t)inner + j];
+    c0[o] = (float)(s + (double)round_bf16(bo[o]));
+  }
+  return 0;
+}

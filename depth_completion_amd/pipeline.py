@@ -16,10 +16,8 @@ Deviations (documented in DESIGN.md):
 """
 from __future__ import annotations
 
-import math
 import os
 
-import numpy as np
 import torch
 
 from . import _lib, ops
@@ -39,40 +37,55 @@ _PROJ = {"linear": 0, "log": 1, "log10": 2}
 
 class DDIMTables:
     """DDIMScheduler(scaled_linear 0.00085..0.012, v_prediction, set_alpha_to_one=False,
-    timestep_spacing="trailing") reduced to per-step scalar tables (fp32, computed as the
-    scheduler does on the CPU)."""
+    timestep_spacing="trailing") reduced to per-step scalar tables: the library's dc_schedule_tables (host CPU
+    code shared with the native session, so both hosts feed the kernels the same bits).  ``config`` mirrors
+    diffusers' scheduler config (``pipe.scheduler.config``, predict.py:491-494)."""
 
-    def __init__(self, num_train_timesteps=1000, beta_start=0.00085, beta_end=0.012):
-        self.T = num_train_timesteps
-        betas = torch.linspace(beta_start ** 0.5, beta_end ** 0.5, self.T, dtype=torch.float32) ** 2
-        self.alphas_cumprod = torch.cumprod(1.0 - betas, dim=0)
-        self.final_alpha_cumprod = self.alphas_cumprod[0]
+    T = 1000
+
+    def __init__(self, config: dict | None = None):
+        cfg = dict(DDIM_CONFIG)
+        cfg.update(config or {})
+        cfg.pop("_class_name", None)
+        cfg.pop("_diffusers_version", None)
+        self.config = cfg
+
+    def check(self) -> None:
+        """The HIP sampler implements the predict.py scheduler (trailing spacing, predict.py:491-494); a checkpoint's
+        shipped config (e.g. timestep_spacing="leading") must be swapped as predict.py does before sampling."""
+        for k, want in DDIM_CONFIG.items():
+            if self.config.get(k, want) != want:
+                raise ValueError(f"scheduler {k}={self.config.get(k)!r} is not supported by the HIP sampler (it "
+                                 f"implements {k}={want!r}, the predict.py configuration: "
+                                 "DDIMScheduler.from_config(pipe.scheduler.config, timestep_spacing='trailing'))")
+
+    def _tables(self, steps: int, lr=(0.05, 0.005), opt: int = 0):
+        self.check()
+        ts = torch.empty(steps, dtype=torch.int64)
+        coef = torch.empty(steps, 4, dtype=torch.float32)
+        adam = torch.empty(steps, 4, dtype=torch.float32)
+        _lib.call("dc_schedule_tables", int(steps), float(lr[0]), float(lr[1]), int(opt), ts.data_ptr(),
+                  coef.data_ptr(), adam.data_ptr())
+        return ts, coef, adam
 
     def timesteps(self, steps: int) -> torch.Tensor:
-        ratio = self.T / steps
-        ts = np.round(np.arange(self.T, 0, -ratio)).astype(np.int64) - 1
-        return torch.from_numpy(ts)
+        return self._tables(steps)[0]
 
     def coef(self, steps: int) -> torch.Tensor:
-        rows = []
-        for t in self.timesteps(steps):
-            a = self.alphas_cumprod[t]
-            prev = int(t) - self.T // steps
-            ap = self.alphas_cumprod[prev] if prev >= 0 else self.final_alpha_cumprod
-            b = 1 - a
-            std = 0.0 * ((1 - ap) / b * (1 - a / ap)) ** 0.5
-            rows.append(torch.stack([a ** 0.5, b ** 0.5, ap ** 0.5, (1 - ap - std ** 2) ** 0.5]))
-        return torch.stack(rows).float()
+        return self._tables(steps)[1]
 
 
-def adam_table(steps: int, lr_latent: float, lr_scaling: float, beta1=0.9, beta2=0.999) -> torch.Tensor:
-    """torch.optim.Adam scalars per step (Python doubles, cast to fp32 as the foreach kernels do)."""
-    rows = []
-    for k in range(1, steps + 1):
-        bc1 = 1 - beta1 ** k
-        bc2 = 1 - beta2 ** k
-        rows.append([lr_latent / bc1, bc2 ** 0.5, lr_scaling / bc1, 0.0])
-    return torch.tensor(rows, dtype=torch.float32)
+# marigold-v1-0 scheduler_config.json with predict.py's timestep_spacing="trailing" override
+DDIM_CONFIG = {"num_train_timesteps": 1000, "beta_start": 0.00085, "beta_end": 0.012, "beta_schedule": "scaled_linear",
+               "prediction_type": "v_prediction", "set_alpha_to_one": False, "steps_offset": 0,
+               "timestep_spacing": "trailing", "clip_sample": False, "thresholding": False,
+               "rescale_betas_zero_snr": False}
+
+
+def adam_table(steps: int, lr_latent: float, lr_scaling: float, opt: int = 0) -> torch.Tensor:
+    """torch.optim.Adam scalars per step (Python doubles, cast to fp32 as the foreach kernels do); opt 1 / 2
+    (SGD / Adagrad): the plain learning rates."""
+    return DDIMTables()._tables(steps, (lr_latent, lr_scaling), opt)[2]
 
 
 class MarigoldDepthCompletionPipeline:
@@ -91,18 +104,94 @@ class MarigoldDepthCompletionPipeline:
         # predict.py:44-52, 483-488: "light" = TAESD (AutoencoderTiny), "original" = the SD AutoencoderKL
         if vae not in ("light", "original"):
             raise ValueError(f"Unknown vae: {vae}")
-        self.vae_kind = vae
-        if vae == "light":
-            self.vae = TAESDHIP(vae_state, self.device)
-        else:
-            self.vae = AutoencoderKLHIP(vae_state, self.device, vae_config or SD_VAE)
-        self.scheduler = DDIMTables()
+        self._set_vae(vae, vae_state, vae_config)
+        self._scheduler = DDIMTables()
         self.empty_text_embedding = text_embedding
         self.use_graph = use_graph
         # sparse-aware decode in the guided step (point losses, TAESD): DC_SPARSE_DECODE=0 disables it
         self.sparse_decode = os.environ.get("DC_SPARSE_DECODE", "1") != "0"
         self._plans = {}
         self.last_loss = None
+
+    # ------------------------------------------------------------------ reference construction surface
+    @classmethod
+    def from_pretrained(cls, path, prediction_type: str | None = "depth", torch_dtype=torch.bfloat16,
+                        device="cuda", **kw):
+        """``MarigoldDepthCompletionPipeline.from_pretrained(ckpt, prediction_type="depth", torch_dtype=dtype)``
+        (predict.py:474-481) over a LOCAL diffusers-layout directory (no hub access): unet/ (+ config.json),
+        vae/ (AutoencoderKL) or taesd/, scheduler/scheduler_config.json, and the empty-prompt embedding
+        (empty_text_embedding.safetensors, or computed once from text_encoder/; pretrained.empty_text_embedding).
+        The scheduler keeps the shipped config until swapped, as predict.py:491-494 does."""
+        from pathlib import Path
+
+        from . import pretrained as pt
+        if prediction_type not in (None, "depth"):
+            raise ValueError(f"prediction_type={prediction_type!r}: the depth-completion sampler is 'depth'")
+        pt._check_dtype(torch_dtype)
+        d = Path(path)
+        unet = pt.UNet2DConditionModel.from_pretrained(d)
+        emb = pt.empty_text_embedding(d)
+        if (d / "vae").exists():
+            vae, kind = pt.AutoencoderKL.from_pretrained(d), "original"
+        elif (d / "taesd").exists():
+            vae, kind = pt.AutoencoderTiny.from_pretrained(d, subfolder="taesd"), "light"
+        else:
+            raise FileNotFoundError(f"{d}: neither vae/ nor taesd/")
+        pipe = cls(unet.state_dict, vae.state_dict, emb, unet_config=unet.unet_config(), device=device, vae=kind,
+                   vae_config=pt.kl_config_from_dict(vae.config) if kind == "original" else None, **kw)
+        if (d / "scheduler" / "scheduler_config.json").exists():
+            pipe.scheduler = pt.DDIMScheduler.from_pretrained(d)
+        return pipe
+
+    def to(self, device=None, *_, **__):
+        """``.to("cuda")`` of predict.py:481: the HIP modules already live on the construction device."""
+        if device is not None and torch.device(device).type != self.device.type:
+            raise ValueError(f"the HIP pipeline lives on {self.device}; it cannot move to {device}")
+        return self
+
+    @property
+    def vae(self):
+        return self._vae
+
+    @vae.setter
+    def vae(self, v):
+        """``pipe.vae = AutoencoderTiny.from_pretrained(VAE_CKPT_LIGHT, torch_dtype=dtype).to("cuda")``
+        (predict.py:484-488): rebuild the HIP VAE from the holder's weights."""
+        from . import pretrained as pt
+        if isinstance(v, pt.AutoencoderTiny):
+            self._set_vae("light", v.state_dict, None)
+        elif isinstance(v, pt.AutoencoderKL):
+            self._set_vae("original", v.state_dict, pt.kl_config_from_dict(v.config))
+        elif isinstance(v, (TAESDHIP, AutoencoderKLHIP)):
+            self._vae, self.vae_kind = v, ("light" if isinstance(v, TAESDHIP) else "original")
+            self._plans = {}
+        else:
+            raise TypeError(f"unsupported vae {type(v).__name__}: AutoencoderTiny / AutoencoderKL "
+                            "(depth_completion_amd.pretrained) or a HIP VAE module")
+
+    def _set_vae(self, kind, state, cfg):
+        self.vae_kind = kind
+        self._vae = TAESDHIP(state, self.device) if kind == "light" else AutoencoderKLHIP(state, self.device,
+                                                                                          cfg or SD_VAE)
+        self._plans = {}
+
+    @property
+    def scheduler(self):
+        return self._scheduler
+
+    @scheduler.setter
+    def scheduler(self, s):
+        """``pipe.scheduler = DDIMScheduler.from_config(pipe.scheduler.config, timestep_spacing="trailing")``
+        (predict.py:491-494); LCMScheduler (--model lcm) is outside the hot path."""
+        from . import pretrained as pt
+        if isinstance(s, pt.LCMScheduler):
+            raise ValueError("LCMScheduler (--model lcm) is not supported by the HIP sampler")
+        if isinstance(s, DDIMTables):
+            self._scheduler = s
+        elif isinstance(s, pt.DDIMScheduler) or hasattr(s, "config"):
+            self._scheduler = DDIMTables(dict(s.config))
+        else:
+            raise TypeError(f"unsupported scheduler {type(s).__name__}")
 
     # ------------------------------------------------------------------ plans
     def _plan(self, nb, h, w):
@@ -289,8 +378,7 @@ class MarigoldDepthCompletionPipeline:
         # ---- per-call tables
         ts = self.scheduler.timesteps(steps)
         coef = self.scheduler.coef(steps).to(dev)
-        adam = (adam_table(steps, lr_latent, lr_scaling) if opt == "adam" else
-                torch.tensor([[lr_latent, 0.0, lr_scaling, 0.0]] * steps, dtype=torch.float32)).to(dev)
+        adam = adam_table(steps, lr_latent, lr_scaling, opt_code).to(dev)
         self.unet.build_temb_tables(ctx, ts)
         for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"], st["daff"]):
             ops.memset(ctx, t)

@@ -9,8 +9,6 @@ hipGraph capture of one guided step needs.  Only the gradient w.r.t. the depth-l
 """
 from __future__ import annotations
 
-import math
-
 import torch
 
 from . import ops
@@ -62,12 +60,13 @@ class TransformerW:
 
 
 def timestep_embedding(timesteps: torch.Tensor, dim: int) -> torch.Tensor:
-    """diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), fp32, host."""
-    half = dim // 2
-    exponent = -math.log(10000) * torch.arange(0, half, dtype=torch.float32) / half
-    emb = timesteps[:, None].float() * torch.exp(exponent)[None, :]
-    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
-    return torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    """diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), fp32, host: the library's
+    dc_timestep_embedding, which the native session (csrc/session.cpp) uses too (same bits on both hosts)."""
+    from . import _lib
+    ts = timesteps.detach().cpu().to(torch.int64).contiguous()
+    out = torch.empty(ts.numel(), dim, dtype=torch.float32)
+    _lib.call("dc_timestep_embedding", ts.data_ptr(), ts.numel(), dim, out.data_ptr())
+    return out
 
 
 class UNetHIP:

@@ -9,8 +9,6 @@ This is a one-time, load-time layout transform (like a checkpoint converter); no
 """
 from __future__ import annotations
 
-import math
-
 import torch
 import torch.nn.functional as F
 
@@ -90,26 +88,22 @@ def fold_cross_attention(sd: dict, pre: str, ctx: torch.Tensor, heads: int):
 
     softmax over 2 keys: p0 = sigmoid(q.(k0-k1)/sqrt(64)); out = v1 + p0 (v0 - v1) per head, so
     attn2(n) = Wo(v1) + bo + sum_h p0_h Wo_h(v0_h - v1_h),  p0_h = sigmoid(n . U_h),
-    U_h = Wq_h^T (k0_h - k1_h) / 8,  D_h = Wo_h (v0_h - v1_h),  c0 = Wo v1 + bo.
-    k, v are rounded to bf16 as the reference computes them (to_k/to_v in bf16).
+    U_h = Wq_h^T (k0_h - k1_h) / 8,  D_h = Wo_h (v0_h - v1_h),  c0 = Wo v1 + bo,
+    in double from the bf16-rounded weights, k and v rounded to bf16 as the reference computes them (to_k / to_v
+    in bf16).  Computed by the library's dc_fold_cross_attention (host code shared with the native session).
     """
-    wq = round_bf16(sd[pre + "to_q.weight"]).double()
-    wk = round_bf16(sd[pre + "to_k.weight"]).double()
-    wv = round_bf16(sd[pre + "to_v.weight"]).double()
-    wo = round_bf16(sd[pre + "to_out.0.weight"]).double()
-    bo = round_bf16(sd[pre + "to_out.0.bias"]).double()
-    c = round_bf16(ctx).double()  # [2][cross]
-    k = round_bf16((c @ wk.t()).float()).double()  # [2][inner]
-    v = round_bf16((c @ wv.t()).float()).double()
-    inner = wq.shape[0]
-    hd = inner // heads
-    C = wq.shape[1]
-    U = torch.zeros(heads, C, dtype=torch.float64)
-    D = torch.zeros(heads, wo.shape[0], dtype=torch.float64)
-    scale = 1.0 / math.sqrt(hd)
-    for h in range(heads):
-        sl = slice(h * hd, (h + 1) * hd)
-        U[h] = wq[sl].t() @ (k[0, sl] - k[1, sl]) * scale
-        D[h] = wo[:, sl] @ (v[0, sl] - v[1, sl])
-    c0 = wo @ v[1] + bo
-    return U.float(), D.float(), c0.float()
+    from . import _lib
+
+    def f32(t):
+        return t.detach().float().contiguous().cpu()
+    wq, wk, wv = f32(sd[pre + "to_q.weight"]), f32(sd[pre + "to_k.weight"]), f32(sd[pre + "to_v.weight"])
+    wo, bo = f32(sd[pre + "to_out.0.weight"]), f32(sd[pre + "to_out.0.bias"])
+    c = f32(ctx.reshape(-1, ctx.shape[-1]))
+    inner, C = wq.shape
+    cout = wo.shape[0]
+    U = torch.empty(heads, C, dtype=torch.float32)
+    D = torch.empty(heads, cout, dtype=torch.float32)
+    c0 = torch.empty(cout, dtype=torch.float32)
+    _lib.call("dc_fold_cross_attention", wq.data_ptr(), wk.data_ptr(), wv.data_ptr(), wo.data_ptr(), bo.data_ptr(),
+              c.data_ptr(), c.shape[0], inner, C, wk.shape[1], cout, heads, U.data_ptr(), D.data_ptr(), c0.data_ptr())
+    return U, D, c0

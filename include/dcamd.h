@@ -267,6 +267,73 @@ long long dc_ensemble_ws_bytes(int frames, long long hw);
 int dc_ensemble_fit(const float* dense, int frames, int seeds, long long hw, const float* guide, float* out,
                     float* affine, void* ws, long long ws_bytes, void* stream);
 
+
+/* ---------------------------------------------------------------- host-side tables (CPU, shared by both hosts)
+ * Computed on the CPU by the library so that the Python host and the native session feed the kernels the same
+ * bits.  dc_schedule_tables: the DDIMScheduler of Marigold v1-0 (scaled_linear betas 0.00085..0.012, v_prediction,
+ * set_alpha_to_one=False) with timestep_spacing="trailing" (predict.py:491-494; marigold_dc.py:800, 823-826,
+ * 902-904): timesteps[steps] (int64), coef[steps][4] as for dc_preview, and adam[steps][4] as for
+ * dc_latent_update (opt 0: torch.optim.Adam bias corrections, marigold_dc.py:783, 897; 1 / 2: [lr_lat, 0,
+ * lr_aff, 0]).  dc_timestep_embedding: diffusers get_timestep_embedding(flip_sin_to_cos=True, shift 0), fp32
+ * out[n][dim] (UNet2DConditionModel.time_proj, marigold_dc.py:459-465).  dc_fold_cross_attention: attn2 of a
+ * BasicTransformerBlock with the constant 2-token empty-prompt context (marigold_dc.py:663-674) folded into
+ * U[heads][c], D[heads][cout], c0[cout]; weights fp32 host arrays in diffusers layout. */
+int dc_schedule_tables(int steps, double lr_latent, double lr_scaling, int opt, long long* timesteps, float* coef,
+                       float* adam);
+int dc_timestep_embedding(const long long* timesteps, int n, int dim, float* out);
+int dc_fold_cross_attention(const float* wq, const float* wk, const float* wv, const float* wo, const float* bo,
+                            const float* ctx, int ntok, int inner, int c, int cross, int cout, int heads, float* U,
+                            float* D, float* c0);
+
+/* ---------------------------------------------------------------- native session
+ * The whole guided sampler behind an opaque handle, for hosts that are not Python: the same weight packing,
+ * buffers and launch sequence as the Python pipeline (results equal bitwise), one guided step captured as a
+ * hipGraph and replayed per timestep.  Replaces MarigoldDepthCompletionPipeline.from_pretrained + __call__
+ * (predict.py:474-503, marigold_dc.py:467-985) for the predict.py default path: guided per-step optimisation
+ * of the latents and the learned affine, l1 + l2 point losses, TAESD; norm const / minmax; any projection,
+ * inv, interpolation and optimiser.  Every call returns a status; dc_session_error() gives the message (the
+ * reference's ValueError text where one applies).  Tensors are device pointers: images uint8 [n][3][H][W],
+ * sparse depth fp32 [n][1][H][W] (0 = missing), latents bf16 [n][4][h][w] (dc_latent_hw), noise bf16
+ * [noise_n][4][h][w] (noise_n 1: one draw shared by every frame, as the reference draws it; n: per frame),
+ * affine fp32 [n][2] (learned scale, shift), dense fp32 [n][1][H][W] metres.  `stream` orders the session's
+ * work after the caller's and the caller's after the session's (the session launches on a stream of its own). */
+typedef struct dc_session dc_session;
+typedef struct dc_sample_params {
+  float max_depth, min_depth;  /* (120, 0): predict.py:101-114 */
+  int norm;                    /* 0 const, 1 minmax */
+  int projection;              /* 0 linear, 1 log, 2 log10 */
+  int inv;
+  int interp;                  /* 0 bilinear, 1 nearest */
+  int steps;                   /* DDIM steps (50) */
+  int resolution;              /* processing resolution (768) */
+  int opt;                     /* 0 Adam, 1 SGD, 2 Adagrad */
+  double lr_latent, lr_scaling;  /* (0.05, 0.005) */
+  float beta;                  /* warm start beta * noise + (1 - beta) * prev (0.9) */
+  int use_graph;               /* 1: replay one captured guided step */
+} dc_sample_params;
+void dc_sample_params_default(dc_sample_params* p);
+int dc_latent_hw(int H, int W, int resolution, int* h, int* w);
+int dc_create(dc_session** out, int device);
+int dc_destroy(dc_session* s);
+const char* dc_session_error(const dc_session* s);
+/* dir: unet/config.json + unet/diffusion_pytorch_model.safetensors, taesd/ (or vae/)
+ * diffusion_pytorch_model.safetensors, empty_text_embedding.safetensors ("embedding" [1][2][cross]);
+ * tuned_table: the GEMM variant table (depth_completion_amd/tuned_gfx950.json) or NULL (library heuristic) */
+int dc_load_weights(dc_session* s, const char* dir, const char* tuned_table);
+/* preprocess + TAESD encoder (marigold_dc.py:687-698) */
+int dc_encode(dc_session* s, const void* imgs_u8, int n, int H, int W, int resolution, void* latents, void* stream);
+/* the guided denoising loop (marigold_dc.py:661-909) from image latents; prev (may be NULL): pred_latents_prev */
+int dc_guided_sample(dc_session* s, const void* img_latents, const void* noise, int noise_n, const void* prev,
+                     const float* sparses, int n, int H, int W, const dc_sample_params* p, void* latents_out,
+                     float* affine_out, void* stream);
+/* final decode + learned-affine de-normalisation (marigold_dc.py:969-985) */
+int dc_decode_dense(dc_session* s, const void* latents, const float* affine, const float* sparses, int n, int H,
+                    int W, const dc_sample_params* p, float* dense_out, void* stream);
+/* all of __call__ (encode + guided sample + final decode); latents_out may be NULL */
+int dc_complete(dc_session* s, const void* imgs_u8, const float* sparses, int n, int H, int W, const void* noise,
+                int noise_n, const void* prev, const dc_sample_params* p, float* dense_out, void* latents_out,
+                void* stream);
+
 #ifdef __cplusplus
 }
 #endif
