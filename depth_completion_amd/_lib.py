@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -52,8 +52,10 @@ _SIGS = {
     "dc_layernorm_bwd": [vp, i32, i64, i32, vp, vp, vp, i32, vp, i32, vp, i32, vp],
     "dc_attn_fwd": [vp, i32, i32, i32, i32, vp, i32, vp, vp, i64, vp],
     "dc_attn_bwd": [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, i32, vp, i64, vp],
-    "dc_crossattn_fwd": [vp, i32, i64, i32, i32, f32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
-    "dc_crossattn_bwd": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, i32, vp],
+    "dc_crossattn_tables_bytes": [i32, i32],
+    "dc_crossattn_prepare": [vp, vp, i32, i32, vp, vp],
+    "dc_crossattn_fwd": [vp, i32, i64, i32, i32, f32, vp, vp, vp, vp, vp, i32, vp, vp, vp],
+    "dc_crossattn_bwd": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, i32, vp, i32, vp],
     "dc_geglu_fwd": [vp, i32, i64, i32, vp, i32, vp],
     "dc_geglu_bwd": [vp, i32, i64, i32, vp, i32, vp, i32, vp],
     "dc_upsample_adjoint": [vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp],
@@ -115,7 +117,7 @@ _SIGS.update({
 })
 _RESTYPE = {"dc_session_error": C.c_char_p, "dc_sample_params_default": None,
             "dc_build_id": C.c_char_p, "dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64,
-             "dc_ensemble_ws_bytes": i64}
+             "dc_ensemble_ws_bytes": i64, "dc_crossattn_tables_bytes": i64}
 
 STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}
 

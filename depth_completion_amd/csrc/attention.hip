@@ -1055,272 +1055,6 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   }
 }
 
-// ------------------------------------------------------------------ folded 2-key cross-attention
-// attn2(LN2(x)) with a constant 2-token context reduces exactly to
-//   out = x + c0 + sum_h sigmoid(LN2(x) . U_h) * D_h        (U, D: [H][C] fp32, c0: [C] fp32)
-// (U_h = Wq_h^T (k1_h - k2_h)/8, D_h = Wo_h (v1_h - v2_h), c0 = Wo v2 + bo).
-// One wave per pixel row, 4 rows per block.  U and D are staged once per block into LDS by LDS-DMA
-// (the per-row head loops would otherwise be chains of dependent L2 round trips), laid out
-// [head][half][vi] so a lane's two float4 of one head are conflict-free ds_read_b128s.  When U and D
-// do not fit together (C 1280 x 20 heads: 2 x 100 KB) the second reuses the first's buffer.
-constexpr int kCrossMaxHeads = 20;  // SD2 UNet: 5 / 10 / 20 heads
-// rows (one per wave) per block: each block stages the whole U / D tables, so the wider levels (10 / 20
-// heads, 26-102 KB per table) stage once per 8 rows (level 2: 27.2 -> 24.6 us fwd), level 0 keeps 4
-template <int MAXV>
-constexpr int kCrossRows = MAXV == 1 ? 4 : 8;
-constexpr int kCrossLdsMax = 160 * 1024;
-
-__host__ __device__ inline int cross_tab_bytes(int heads, int c) { return ((heads * c * 4 + 1023) / 1024) * 1024; }
-
-// stage one [heads][c] fp32 table into LDS as [head][half][vi] (16 B pieces), all waves issuing
-__device__ __forceinline__ void cross_stage(const float* tab, int heads, int nv, char* lds) {
-  const __amdgpu_buffer_rsrc_t r = buf_rsrc(tab);
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int np = heads * nv * 2;
-  const int nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
-  for (int j = wv; j * 64 < np; j += nw) {
-    const int pc = j * 64 + lane;
-    const int hd = pc / (2 * nv), rem = pc - hd * 2 * nv;
-    const int half = rem >= nv ? 1 : 0, vi = rem - half * nv;
-    buf_load_lds16(r, (DC_LDS char*)lds + j * 1024, pc < np ? (hd * 2 * nv + vi * 2 + half) * 16 : kOOB, 0);
-  }
-}
-__device__ __forceinline__ void cross_read(const char* lds, int hd, int nv, int vi, float4& a, float4& b) {
-  a = *reinterpret_cast<const float4*>(lds + ((hd * 2) * nv + vi) * 16);
-  b = *reinterpret_cast<const float4*>(lds + ((hd * 2 + 1) * nv + vi) * 16);
-}
-
-template <int MAXV>
-__global__ __launch_bounds__(64 * kCrossRows<MAXV>) void cross_fwd_kernel(const bf16* x, int ldx, long rows, int c,
-                                                                    int heads, float eps, const float* gamma,
-                                                                    const float* beta, const float* U, const float* D,
-                                                                    const float* c0, bf16* y, int ldy, float* stats,
-                                                                    float* probs) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const long row = (long)blockIdx.x * kCrossRows<MAXV> + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const bool ok = row < rows;
-  const int nv = c >> 3;
-  const int tb = cross_tab_bytes(heads, c);
-  const bool both = 2 * tb <= kCrossLdsMax;
-  char* lu = lds;
-  char* ld_ = both ? lds + tb : lds;
-  cross_stage(U, heads, nv, lu);
-  if (both) cross_stage(D, heads, nv, ld_);
-  float xv[MAXV][8], nn[MAXV][8];
-  float s = 0.0f;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (ok && vi < nv) {
-      load8(x + row * ldx + vi * 8, xv[k]);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s += xv[k][i];
-    }
-  }
-  const float mu = wave_sum(s) / c;
-  float q = 0.0f;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (ok && vi < nv) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { const float d = xv[k][i] - mu; q += d * d; }
-    }
-  }
-  const float rs = rsqrtf(wave_sum(q) / c + eps);
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (ok && vi < nv) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        nn[k][i] = (float)(bf16)((xv[k][i] - mu) * rs * gamma[vi * 8 + i] + beta[vi * 8 + i]);
-    }
-  }
-  vm_wait_n<0>();
-  __syncthreads();
-  // all heads' logits in one pass over the row, reduced together (independent butterflies), then the
-  // sigmoid-weighted sum of the D rows
-  float d[kCrossMaxHeads];
-#pragma unroll
-  for (int hd = 0; hd < kCrossMaxHeads; ++hd) d[hd] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (ok && vi < nv) {
-#pragma unroll
-      for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
-        if (hd < heads) {
-          float4 u0, u1;
-          cross_read(lu, hd, nv, vi, u0, u1);
-          d[hd] += nn[k][0] * u0.x + nn[k][1] * u0.y + nn[k][2] * u0.z + nn[k][3] * u0.w + nn[k][4] * u1.x +
-                   nn[k][5] * u1.y + nn[k][6] * u1.z + nn[k][7] * u1.w;
-        }
-      }
-    }
-  }
-  if (!both) {  // D replaces U once every wave has its logits
-    __syncthreads();
-    cross_stage(D, heads, nv, ld_);
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-    for (int hd = 0; hd < kCrossMaxHeads; ++hd)
-      if (hd < heads) d[hd] += __shfl_xor(d[hd], o, 64);
-  if (!both) {
-    vm_wait_n<0>();
-    __syncthreads();
-  }
-  if (!ok) return;
-  float acc[MAXV][8];
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[k][i] = 0.0f;
-#pragma unroll
-  for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
-    if (hd < heads) {
-      const float p = 1.0f / (1.0f + __expf(-d[hd]));
-      if (lane == 0) probs[row * heads + hd] = p;
-#pragma unroll
-      for (int k = 0; k < MAXV; ++k) {
-        const int vi = lane + 64 * k;
-        if (vi < nv) {
-          float4 d0, d1;
-          cross_read(ld_, hd, nv, vi, d0, d1);
-          acc[k][0] += p * d0.x; acc[k][1] += p * d0.y; acc[k][2] += p * d0.z; acc[k][3] += p * d0.w;
-          acc[k][4] += p * d1.x; acc[k][5] += p * d1.y; acc[k][6] += p * d1.z; acc[k][7] += p * d1.w;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (vi < nv) {
-      float o[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)(acc[k][i] + c0[vi * 8 + i]) + xv[k][i];
-      store8(y + row * ldy + vi * 8, o);
-    }
-  }
-  if (lane == 0) {
-    stats[row * 2] = mu;
-    stats[row * 2 + 1] = rs;
-  }
-}
-
-template <int MAXV>
-__global__ __launch_bounds__(64 * kCrossRows<MAXV>) void cross_bwd_kernel(const bf16* x, int ldx, long rows, int c,
-                                                                    int heads, const float* gamma, const float* U,
-                                                                    const float* D, const float* stats,
-                                                                    const float* probs, const bf16* dy, int lddy,
-                                                                    bf16* dx, int lddx) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const long row = (long)blockIdx.x * kCrossRows<MAXV> + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const bool ok = row < rows;
-  const int nv = c >> 3;
-  const int tb = cross_tab_bytes(heads, c);
-  const bool both = 2 * tb <= kCrossLdsMax;
-  char* ld_ = lds;
-  char* lu = both ? lds + tb : lds;
-  cross_stage(D, heads, nv, ld_);
-  if (both) cross_stage(U, heads, nv, lu);
-  float dv[MAXV][8], dn[MAXV][8];
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) dn[k][i] = 0.0f;
-    if (ok && vi < nv) load8(dy + row * lddy + vi * 8, dv[k]);
-  }
-  vm_wait_n<0>();
-  __syncthreads();
-  float d[kCrossMaxHeads];
-#pragma unroll
-  for (int hd = 0; hd < kCrossMaxHeads; ++hd) d[hd] = 0.0f;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (ok && vi < nv) {
-#pragma unroll
-      for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
-        if (hd < heads) {
-          float4 d0, d1;
-          cross_read(ld_, hd, nv, vi, d0, d1);
-          d[hd] += dv[k][0] * d0.x + dv[k][1] * d0.y + dv[k][2] * d0.z + dv[k][3] * d0.w + dv[k][4] * d1.x +
-                   dv[k][5] * d1.y + dv[k][6] * d1.z + dv[k][7] * d1.w;
-        }
-      }
-    }
-  }
-  if (!both) {
-    __syncthreads();
-    cross_stage(U, heads, nv, lu);
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-    for (int hd = 0; hd < kCrossMaxHeads; ++hd)
-      if (hd < heads) d[hd] += __shfl_xor(d[hd], o, 64);
-  if (!both) {
-    vm_wait_n<0>();
-    __syncthreads();
-  }
-  if (!ok) return;
-#pragma unroll
-  for (int hd = 0; hd < kCrossMaxHeads; ++hd) {
-    if (hd < heads) {
-      const float p = probs[row * heads + hd];
-      const float dsg = d[hd] * p * (1.0f - p);
-#pragma unroll
-      for (int k = 0; k < MAXV; ++k) {
-        const int vi = lane + 64 * k;
-        if (vi < nv) {
-          float4 u0, u1;
-          cross_read(lu, hd, nv, vi, u0, u1);
-          dn[k][0] += dsg * u0.x; dn[k][1] += dsg * u0.y; dn[k][2] += dsg * u0.z; dn[k][3] += dsg * u0.w;
-          dn[k][4] += dsg * u1.x; dn[k][5] += dsg * u1.y; dn[k][6] += dsg * u1.z; dn[k][7] += dsg * u1.w;
-        }
-      }
-    }
-  }
-  // LayerNorm backward of dn, plus the residual path
-  const float mu = stats[row * 2], rs = stats[row * 2 + 1];
-  float xh[MAXV][8];
-  float sa = 0.0f, sb = 0.0f;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (vi < nv) {
-      float f[8];
-      load8(x + row * ldx + vi * 8, f);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        xh[k][i] = (f[i] - mu) * rs;
-        dn[k][i] = (float)(bf16)dn[k][i] * gamma[vi * 8 + i];
-        sa += dn[k][i];
-        sb += dn[k][i] * xh[k][i];
-      }
-    }
-  }
-  const float ma = wave_sum(sa) / c, mb = wave_sum(sb) / c;
-#pragma unroll
-  for (int k = 0; k < MAXV; ++k) {
-    const int vi = lane + 64 * k;
-    if (vi < nv) {
-      float o[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)(rs * (dn[k][i] - ma - xh[k][i] * mb)) + dv[k][i];
-      store8(dx + row * lddx + vi * 8, o);
-    }
-  }
-}
-
 }  // namespace
 
 namespace {
@@ -1483,50 +1217,6 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
     case 1: launch_bwd<4, 2>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
     default: launch_bwd<2, 2>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
   }
-  DC_CHECK_LAUNCH();
-  return DC_OK;
-}
-
-#define DC_CROSS_DISPATCH(KER, ...)                                                            \
-  do {                                                                                         \
-    const int nv = c / 8;                                                                      \
-    const int tb = cross_tab_bytes(heads, c);                                                  \
-    const size_t lds = 2 * tb <= kCrossLdsMax ? 2 * tb : tb;                                   \
-    if (tb > kCrossLdsMax) return DC_ERR_ARG;                                                  \
-    auto grid = [&](int r) { return dim3((unsigned)((rows + r - 1) / r)); };                  \
-    hipStream_t st = (hipStream_t)stream;                                                      \
-    if (nv <= 64)                                                                              \
-      hipLaunchKernelGGL(KER<1>, grid(kCrossRows<1>), dim3(64 * kCrossRows<1>), lds, st, __VA_ARGS__); \
-    else if (nv <= 192)                                                                        \
-      hipLaunchKernelGGL(KER<3>, grid(kCrossRows<3>), dim3(64 * kCrossRows<3>), lds, st, __VA_ARGS__); \
-    else if (nv <= 320)                                                                        \
-      hipLaunchKernelGGL(KER<5>, grid(kCrossRows<5>), dim3(64 * kCrossRows<5>), lds, st, __VA_ARGS__); \
-    else                                                                                       \
-      return DC_ERR_ARG;                                                                       \
-  } while (0)
-
-extern "C" int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps,
-                                const float* gamma, const float* beta, const float* U, const float* D,
-                                const float* c0, void* y, int ldy, float* stats, float* probs, void* stream) {
-  if (!x || !y || !gamma || !beta || !U || !D || !c0 || !stats || !probs || rows <= 0 || c % 8 || heads <= 0 ||
-      heads > kCrossMaxHeads)
-    return DC_ERR_ARG;
-  if (ldx % 8 || ldy % 8) return DC_ERR_ALIGN;
-  DC_CROSS_DISPATCH(cross_fwd_kernel, (const bf16*)x, ldx, (long)rows, c, heads, eps, gamma, beta, U, D, c0, (bf16*)y,
-                    ldy, stats, probs);
-  DC_CHECK_LAUNCH();
-  return DC_OK;
-}
-
-extern "C" int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, int heads, const float* gamma,
-                                const float* U, const float* D, const float* stats, const float* probs,
-                                const void* dy, int lddy, void* dx, int lddx, void* stream) {
-  if (!x || !dy || !dx || !gamma || !U || !D || !stats || !probs || rows <= 0 || c % 8 || heads <= 0 ||
-      heads > kCrossMaxHeads)
-    return DC_ERR_ARG;
-  if (ldx % 8 || lddy % 8 || lddx % 8) return DC_ERR_ALIGN;
-  DC_CROSS_DISPATCH(cross_bwd_kernel, (const bf16*)x, ldx, (long)rows, c, heads, gamma, U, D, stats, probs,
-                    (const bf16*)dy, lddy, (bf16*)dx, lddx);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

@@ -54,7 +54,21 @@ struct ConvGemmParams {
   int ldaux;
   const int* rows;      // optional: GEMM row m computes output pixel rows[m] (sorted), nrows of them
   long nrows;
+  int nmajor;           // tile order within an XCD's range: 0 M-major (row tiles share A), 1 N-major (column
+                        // tiles share W; opt-in, DC_GEMM_ORDER=2)
 };
+
+// tile index -> (row tile, column tile) in the launch's rasterisation order
+__device__ __forceinline__ void tile_coords(const ConvGemmParams& p, int tile, int tiles_m, int tiles_n, int& tm,
+                                            int& tn) {
+  if (p.nmajor) {
+    tn = tile / tiles_m;
+    tm = tile - tn * tiles_m;
+  } else {
+    tm = tile / tiles_n;
+    tn = tile - tm * tiles_n;
+  }
+}
 
 // GEMM rows of the launch, and the output pixel of GEMM row m (m < conv_rows(p))
 __device__ __forceinline__ long conv_rows(const ConvGemmParams& p) {
@@ -577,8 +591,22 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     // fetched from HBM once); unsplit, each XCD gets a contiguous run of row tiles.
     const int tiles = gridDim.x, nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int wk = xcd_remap(bid, nblk);
-    const int split = wk / tiles, lb = wk - split * tiles;
-    const int tm = lb / tiles_n, tn = lb - tm * tiles_n;
+    const int tiles_m = tiles / tiles_n;
+    int split, lb, tm, tn;
+    if (p.nmajor) {
+      // (column tile, split, row tile) with the row tile fastest: an XCD's contiguous range shares each (tn, split)
+      // slice of W across all row tiles, so every weight byte leaves HBM for one XCD only
+      tm = wk % tiles_m;
+      const int rest = wk / tiles_m;
+      split = rest % p.splits;
+      tn = rest / p.splits;
+      lb = tm * tiles_n + tn;
+    } else {
+      split = wk / tiles;
+      lb = wk - split * tiles;
+      tm = lb / tiles_n;
+      tn = lb - tm * tiles_n;
+    }
     const long m0 = (long)tm * BM;
     const int n0 = tn * BN;
     const int kc_begin = split * p.kps;
@@ -605,7 +633,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     const int tile = (int)(it / nk);
     const int kb = (int)(it - (long)tile * nk);
     const int ke = (int)min((long)nk, kb + (end - it));
-    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    int tm, tn;
+    tile_coords(p, tile, p.splits / tiles_n, tiles_n, tm, tn);
     const long m0 = (long)tm * BM;
     const int n0 = tn * BN;
     tile_pass<BM, BN, BK, S, SMALLC>(p, smem, m0, n0, kb, ke, acc);
@@ -727,6 +756,13 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   p.y2 = (bf16*)d->y2; p.ldy2 = d->ldy2;
   p.aux = (const bf16*)d->aux; p.ldaux = d->ldaux;
   p.rows = d->rows; p.nrows = d->rows ? d->nrows : 0;
+  // tile order: M-major (split-major for split-K).  N-major -- (column tile, split, row tile), each XCD's range
+  // sharing W slices -- measured no better on the weight-heavy level-2 / 3 shapes and 1.5x slower at batch 8
+  // (profiles/r02f/gemm_order_ab.txt); kept opt-in for experiments (DC_GEMM_ORDER=2)
+  {
+    const char* e = getenv("DC_GEMM_ORDER");
+    p.nmajor = (e && atoi(e) == 2) ? 1 : 0;
+  }
   if (p.geglu < 0 || p.geglu > 2) return DC_ERR_ARG;
   if (p.rows && (p.nrows <= 0 || p.geglu)) return DC_ERR_ARG;
   if (p.geglu) {  // plain linear / conv output only: no residual, mask, row bias or activation

@@ -458,6 +458,7 @@ struct TransformerW {
   NormW norm, ln1, ln2, ln3;
   LinearW proj_in, proj_out, qkv, out, ff1, ff2;
   float *U = nullptr, *D = nullptr, *c0 = nullptr;
+  void* tabs = nullptr;  // MFMA operand tables of the folded cross-attention (dc_crossattn_prepare)
 };
 
 struct UNetW {
@@ -531,6 +532,9 @@ TransformerW load_transformer(Loader& L, const std::string& pre, int heads, cons
   t.U = L.mem().upload(U);
   t.D = L.mem().upload(D);
   t.c0 = L.mem().upload(c0);
+  t.tabs = L.mem().alloc((size_t)dc_crossattn_tables_bytes(heads, C), false);
+  DCK(dc_crossattn_prepare(t.U, t.D, heads, C, t.tabs, nullptr));
+  HIPK(hipDeviceSynchronize());
   // GEGLU projection with (h, gate) rows interleaved 8 + 8 (weights.geglu_interleave)
   HostTensor f1 = st.get(b + "ff.net.0.proj.weight"), f1b = st.get(b + "ff.net.0.proj.bias");
   const int nout = (int)f1.shape[0], kin = (int)f1.shape[1], inner_ff = nout / 2;
@@ -697,7 +701,7 @@ class UNetPlan {
       ex.linear(l1, tp->qkv.wf, tp->qkv.cin, P, 3 * C, qkv);
       DCK(dc_attn_fwd(qkv.p, qkv.ld, nb, T, H, o.p, o.ld, lse, ex.ws, ex.ws_bytes, ex.stream));
       ex.linear(o, tp->out.wf, tp->out.cin, P, C, r1, tp->out.bias, p);
-      DCK(dc_crossattn_fwd(r1.p, r1.ld, P, C, H, tp->ln2.eps, tp->ln2.gamma, tp->ln2.beta, tp->U, tp->D, tp->c0, r2.p,
+      DCK(dc_crossattn_fwd(r1.p, r1.ld, P, C, H, tp->ln2.eps, tp->ln2.gamma, tp->ln2.beta, tp->tabs, tp->c0, r2.p,
                            r2.ld, sl2, probs, ex.stream));
       DCK(dc_layernorm_fwd(r2.p, r2.ld, P, C, tp->ln3.eps, tp->ln3.gamma, tp->ln3.beta, l3.p, l3.ld, sl3, ex.stream));
       ex.linear(l3, tp->ff1.wf, tp->ff1.cin, P, 8 * C, f8, tp->ff1.bias, RB(), nullptr, 0, 1, gg);
@@ -969,7 +973,7 @@ class UNetPlan {
       ex.linear(df, t->ff1.wd, t->ff1.cout, P, C, dl3);
       DCK(dc_layernorm_bwd(r2.p, r2.ld, P, C, t->ln3.gamma, sl3, dl3.p, dl3.ld, dr2.p, dr2.ld, dr3.p, dr3.ld,
                            ex.stream));
-      DCK(dc_crossattn_bwd(r1.p, r1.ld, P, C, H, t->ln2.gamma, t->U, t->D, sl2, probs, dr2.p, dr2.ld, dr1.p, dr1.ld,
+      DCK(dc_crossattn_bwd(r1.p, r1.ld, P, C, H, t->ln2.gamma, t->tabs, sl2, probs, dr2.p, dr2.ld, dr1.p, dr1.ld,
                            ex.stream));
       ex.linear(dr1, t->out.wd, t->out.cout, P, C, dob);
       DCK(dc_attn_bwd(qkv.p, qkv.ld, o.p, o.ld, dob.p, dob.ld, lse, nb, T, H, delta, dqkv.p, dqkv.ld, ex.ws,

@@ -254,15 +254,23 @@ def attn_bwd(ctx: Ctx, qkv, o, dout, lse, nb, t, heads, delta, dqkv):
     return dqkv
 
 
-def crossattn_fwd(ctx: Ctx, x, rows, c, heads, eps, gamma, beta, U, D, c0, y, stats, probs):
-    call("dc_crossattn_fwd", P(x), LD(x), rows, c, heads, eps, gamma.data_ptr(), beta.data_ptr(), U.data_ptr(),
-         D.data_ptr(), c0.data_ptr(), P(y), LD(y), stats.data_ptr(), probs.data_ptr(), ctx.stream)
+def crossattn_tables(ctx: Ctx, U, D, heads, c) -> torch.Tensor:
+    """bf16 hi / lo MFMA operand tables of the folded cross-attention (dc_crossattn_prepare), once at load."""
+    nbytes = _lib.load().dc_crossattn_tables_bytes(heads, c)
+    tabs = torch.empty(nbytes // 2, dtype=BF16, device=ctx.device)
+    call("dc_crossattn_prepare", U.data_ptr(), D.data_ptr(), heads, c, tabs.data_ptr(), ctx.stream)
+    return tabs
+
+
+def crossattn_fwd(ctx: Ctx, x, rows, c, heads, eps, gamma, beta, tabs, c0, y, stats, probs):
+    call("dc_crossattn_fwd", P(x), LD(x), rows, c, heads, eps, gamma.data_ptr(), beta.data_ptr(), tabs.data_ptr(),
+         c0.data_ptr(), P(y), LD(y), stats.data_ptr(), probs.data_ptr(), ctx.stream)
     return y
 
 
-def crossattn_bwd(ctx: Ctx, x, rows, c, heads, gamma, U, D, stats, probs, dy, dx):
-    call("dc_crossattn_bwd", P(x), LD(x), rows, c, heads, gamma.data_ptr(), U.data_ptr(), D.data_ptr(),
-         stats.data_ptr(), probs.data_ptr(), P(dy), LD(dy), P(dx), LD(dx), ctx.stream)
+def crossattn_bwd(ctx: Ctx, x, rows, c, heads, gamma, tabs, stats, probs, dy, dx):
+    call("dc_crossattn_bwd", P(x), LD(x), rows, c, heads, gamma.data_ptr(), tabs.data_ptr(), stats.data_ptr(),
+         probs.data_ptr(), P(dy), LD(dy), P(dx), LD(dx), ctx.stream)
     return dx
 
 

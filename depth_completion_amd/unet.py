@@ -52,6 +52,7 @@ class TransformerW:
         self.out = Linear(sd[b + "attn1.to_out.0.weight"], sd[b + "attn1.to_out.0.bias"], dev)
         U, D, c0 = fold_cross_attention(sd, b + "attn2.", ctx, heads)
         self.U, self.D, self.c0 = U.to(dev), D.to(dev), c0.to(dev)
+        self.cross_tabs = None  # MFMA operand tables (ops.crossattn_tables), built with the first context
         # GEGLU projection with (h, gate) rows interleaved 8 + 8 for the fused epilogues (geglu_interleave)
         perm = geglu_interleave(sd[b + "ff.net.0.proj.weight"].shape[0])
         self.ff1 = Linear(sd[b + "ff.net.0.proj.weight"][perm], sd[b + "ff.net.0.proj.bias"][perm], dev)
@@ -219,6 +220,8 @@ class UNetPlan:
         T = hh * ww
         P = nb * T
         C, H = t.c, t.heads
+        if t.cross_tabs is None:
+            t.cross_tabs = ops.crossattn_tables(ctx, t.U, t.D, H, C)
         n0 = self.buf(P, C)
         st0 = self.fbuf(nb, 32, 2)
         p = self.buf(P, C)
@@ -245,7 +248,8 @@ class UNetPlan:
             ops.linear(ctx, l1, t.qkv.wf, P, 3 * C, qkv)
             ops.attn_fwd(ctx, qkv, nb, T, H, o, lse)
             ops.linear(ctx, o, t.out.wf, P, C, r1, bias=t.out.bias, resid=p)
-            ops.crossattn_fwd(ctx, r1, P, C, H, t.ln2.eps, t.ln2.gamma, t.ln2.beta, t.U, t.D, t.c0, r2, sl2, probs)
+            ops.crossattn_fwd(ctx, r1, P, C, H, t.ln2.eps, t.ln2.gamma, t.ln2.beta, t.cross_tabs, t.c0, r2, sl2,
+                              probs)
             ops.layernorm(ctx, r2, P, C, t.ln3.gamma, t.ln3.beta, t.ln3.eps, l3, sl3)
             ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias, geglu=1, y2=gg)   # + GEGLU
             ops.linear(ctx, gg, t.ff2.wf, P, C, r3, bias=t.ff2.bias, resid=r2)
@@ -469,7 +473,7 @@ class UNetPlan:
             ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, df, geglu=2, aux=f8)   # + GEGLU backward
             ops.linear(ctx, df, t.ff1.wd, P, C, dl3)
             ops.layernorm_bwd(ctx, r2, P, C, t.ln3.gamma, sl3, dl3, dr2, add=dr3)
-            ops.crossattn_bwd(ctx, r1, P, C, H, t.ln2.gamma, t.U, t.D, sl2, probs, dr2, dr1)
+            ops.crossattn_bwd(ctx, r1, P, C, H, t.ln2.gamma, t.cross_tabs, sl2, probs, dr2, dr1)
             ops.linear(ctx, dr1, t.out.wd, P, C, do)
             ops.attn_bwd(ctx, qkv, o, do, lse, nb, T, H, delta, dqkv)
             ops.linear(ctx, dqkv, t.qkv.wd, P, C, dl1)

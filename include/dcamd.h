@@ -103,12 +103,18 @@ int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int 
                 long long ws_bytes, void* stream);
 int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, const void* dout, int lddo, const float* lse, int nb,
                 int t, int heads, float* delta_ws, void* dqkv, int ldd, float* ws, long long ws_bytes, void* stream);
+/* folded cross-attention on MFMA (csrc/crossattn.hip): U, D fp32 [heads][c] (dc_fold_cross_attention) are
+ * prepared once into bf16 hi / lo MFMA operand tables of dc_crossattn_tables_bytes(heads, c) bytes; heads <= 32,
+ * c % 32 == 0, c <= 1280.  stats [rows][2] (mean, rstd of norm2), probs [rows][heads] (the sigmoids) are kept
+ * for the backward. */
+long long dc_crossattn_tables_bytes(int heads, int c);
+int dc_crossattn_prepare(const float* U, const float* D, int heads, int c, void* tabs, void* stream);
 int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps, const float* gamma,
-                     const float* beta, const float* U, const float* D, const float* c0, void* y, int ldy,
-                     float* stats, float* probs, void* stream);
-int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, int heads, const float* gamma, const float* U,
-                     const float* D, const float* stats, const float* probs, const void* dy, int lddy, void* dx,
-                     int lddx, void* stream);
+                     const float* beta, const void* tabs, const float* c0, void* y, int ldy, float* stats,
+                     float* probs, void* stream);
+int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, int heads, const float* gamma, const void* tabs,
+                     const float* stats, const float* probs, const void* dy, int lddy, void* dx, int lddx,
+                     void* stream);
 
 /* ---------------------------------------------------------------- elementwise
  * GEGLU (FeedForward.net[0]), nearest-upsample adjoint (Upsample2D / TAESD Upsample backward),

@@ -423,12 +423,27 @@ def test_cross_attention_fold(ctx, C, heads):
     st = torch.empty(rows, 2, device=dev)
     pr = torch.empty(rows, heads, device=dev)
     xb = x.detach().to(torch.bfloat16)
-    ops.crossattn_fwd(ctx, xb, rows, C, heads, 1e-5, gamma, beta, U, D, c0, y, st, pr)
+    tabs = ops.crossattn_tables(ctx, U, D, heads, C)
+    ops.crossattn_fwd(ctx, xb, rows, C, heads, 1e-5, gamma, beta, tabs, c0, y, st, pr)
     dx = torch.empty_like(y)
-    ops.crossattn_bwd(ctx, xb, rows, C, heads, gamma, U, D, st, pr, dy.to(torch.bfloat16), dx)
+    ops.crossattn_bwd(ctx, xb, rows, C, heads, gamma, tabs, st, pr, dy.to(torch.bfloat16), dx)
     torch.cuda.synchronize()
     assert rel(y, out) < 1e-2
     assert rel(dx, x.grad) < 2e-2
+    # against the fold itself in fp32 with the kernel's bf16 rounding points (LN output, the residual sums): the
+    # MFMA form's hi / lo bf16 operands keep ~16 mantissa bits of U, D and the sigmoids (the reference's LN
+    # statistics sum in another order, so a few bf16-rounded LN outputs land one ulp apart: probs to 2e-3)
+    xf = xb.float()
+    mu = xf.mean(1, keepdim=True)
+    rs = torch.rsqrt(((xf - mu) ** 2).mean(1, keepdim=True) + 1e-5)
+    n = ((xf - mu) * rs * gamma + beta).to(torch.bfloat16).float()
+    p = torch.sigmoid(n @ U.t())
+    yf = ((p @ D + c0).to(torch.bfloat16).float() + xf)
+    torch.testing.assert_close(pr, p, rtol=0, atol=2e-3)
+    assert (pr - p).abs().mean() < 2e-5
+    torch.testing.assert_close(st[:, 0], mu[:, 0], rtol=0, atol=1e-5)
+    assert (y.float() - yf).abs().max() <= 4 * (yf.abs().max() * 2 ** -8)   # within a few bf16 ulps
+    assert rel(y, yf) < 2e-3
 
 
 # ----------------------------------------------------------------------------- elementwise
