@@ -211,6 +211,8 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
+  // wave index as a scalar: the LDS-DMA destination (M0) of every piece is then SALU arithmetic
+  const int wid_s = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long hwo = (long)p.hout * p.wout;
   const long M = conv_rows(p);
   const int nkc = max(0, kc_end - kc_begin);
@@ -346,11 +348,11 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
       if (q_c >= p.c1) {  // uniform: the chunk comes from the second concat source
 #pragma unroll
         for (int j = 0; j < AP; ++j)
-          buf_load_lds16(ra2, sbase + (wid * 64 + 256 * j) * 16, a_off2[j], (q_c - p.c1) * 2);
+          buf_load_lds16(ra2, sbase + (wid_s * 64 + 256 * j) * 16, a_off2[j], (q_c - p.c1) * 2);
       } else {
 #pragma unroll
         for (int j = 0; j < AP; ++j)
-          buf_load_lds16(ra, sbase + (wid * 64 + 256 * j) * 16, a_off[j], q_c * 2);
+          buf_load_lds16(ra, sbase + (wid_s * 64 + 256 * j) * 16, a_off[j], q_c * 2);
       }
     } else {
 #pragma unroll
@@ -363,12 +365,12 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
         const int pix = (ky == 0 ? rt[j].y0 : (ky == 1 ? rt[j].y1 : rt[j].y2)) +
                         (kx == 0 ? rt[j].x0 : (kx == 1 ? rt[j].x1 : rt[j].x2));
         const bf16* src = ok ? p.x + (long)pix * p.ldx + c : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, sbase + (wid * 64 + 256 * j) * 16, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)src, sbase + (wid_s * 64 + 256 * j) * 16, 16, 0, 0);
       }
     }
 #pragma unroll
     for (int j = 0; j < BP; ++j)
-      buf_load_lds16(rb, sbase + BM * RB + (wid * 64 + 256 * j) * 16, b_off[j], q_k * BK * 2);
+      buf_load_lds16(rb, sbase + BM * RB + (wid_s * 64 + 256 * j) * 16, b_off[j], q_k * BK * 2);
     ++q_k;
     if (!SMALLC) {
       q_c += BK;
@@ -387,7 +389,9 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
 
   for (int s = 0; s < S - 1 && s < nkc; ++s) issue(s);
   for (int i = 0; i < nkc; ++i) {
-    wait_chunks<L, S>(min(S - 2, nkc - 1 - i));
+    // steady state: S - 2 younger chunks stay in flight (one compare instead of the wait cascade)
+    if (i + S - 2 < nkc) vm_wait<(S - 2) * L>();
+    else wait_chunks<L, S>(nkc - 1 - i);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
