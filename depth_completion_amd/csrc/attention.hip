@@ -347,6 +347,7 @@ __device__ __forceinline__ bool sk_handoff_fwd(const AttnSK& sk, char* smem, lon
 // for the same 32 QW queries, then the partial (m, l, O) are merged through LDS in a fixed order.
 // K / V tiles stream through an S-deep LDS-DMA ring per split (one barrier per tile).
 constexpr int FWD_S = 3;
+constexpr float FWD_TAU = 8.0f;  // lazy-rescale slack (natural-log units of the scaled scores)
 template <int QW, int KS>
 struct FwdLds {
   static constexpr int STAGE = 2 * TILE_B;                      // K + V
@@ -374,11 +375,19 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
   for (int s = 0; s < 4; ++s) qf[s] = load_row8(base + (long)my_q * ld + h * 64 + 16 * s + 8 * hh, qok, 0.125f);
 
   float m = -INFINITY, l = 0.0f;
-  f32x16 oacc[2];
+  f32x16 oacc[2], lacc;
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[db][r] = 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lacc[r] = 0.0f;
+  // row sums on the MFMA pipe (the softmax is VALU-issue bound, the MFMAs are not): a ones A-operand
+  // against the P fragment gives sum_k P[q][k] in every element of lane q's accumulator, summed from
+  // the same bf16 P the P.V product uses
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
 
   const int per = (tcount + KS - 1) / KS;
   const int tb = t0 + part * per;
@@ -447,27 +456,24 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[b][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      const float ml = mnew * LOG2E;
-      float ps = 0.0f;
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
-          sacc[b][r] = pv;
-          ps += pv;
-        }
-      if (__any(mnew > m)) {
+      // lazy rescale: the reference max moves only when a row max exceeds it by more than FWD_TAU, so
+      // weights stay <= e^FWD_TAU (exact in fp32 / bf16 relative terms; O and l share the reference)
+      if (__any(mx > m + FWD_TAU)) {
+        const float mnew = fmaxf(m, mx);
         const float alpha = fast_exp2((m - mnew) * LOG2E);
-        l *= alpha;
 #pragma unroll
         for (int db = 0; db < 2; ++db)
 #pragma unroll
           for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lacc[r] *= alpha;
+        m = mnew;
       }
-      l += ps;
-      m = mnew;
+      const float ml = m * LOG2E;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[b][r] = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
       // V^T fragments: two k-slices in flight ahead of the MFMAs that consume them
       constexpr int VIMM = ST * FwdLds<QW, KS>::STAGE + TILE_B;
       bf16x8 vf[4][2];
@@ -490,6 +496,7 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
 #pragma unroll
         for (int db = 0; db < 2; ++db)
           oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], pf, oacc[db], 0, 0, 0);
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf, lacc, 0, 0, 0);
       }
     }
   };
@@ -501,6 +508,7 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
   }
   vm_wait_n<0>();
   __syncthreads();
+  l = lacc[0];  // the full row sum (both lane halves of the row hold it)
   if constexpr (KS > 1) {
     // merge the key-split partials: parts 1.. publish (m, l, O) per lane, part 0 folds them in order
     float* red = reinterpret_cast<float*>(smem);
@@ -548,7 +556,7 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
         for (int r = 0; r < 16; ++r) oacc[db][r] = v[2 + 16 * db + r];
     }
   }
-  const float lsum = l + __shfl_xor(l, 32, 64);
+  const float lsum = l;
   const float inv = 1.0f / lsum;
   if (qok) {
     bf16* orow = o + ((long)n * T + my_q) * ldo + h * 64;
