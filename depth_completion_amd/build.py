@@ -25,7 +25,7 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-re
 
 def source_files() -> list[Path]:
     """Every file libdcamd.so is compiled from (the build id hashes exactly these)."""
-    return [CSRC / s for s in SOURCES] + [CSRC / "common.h", CSRC / "json_mini.h", PKG.parent / "include" / "dcamd.h"]
+    return [CSRC / s for s in SOURCES] + [CSRC / "common.h", CSRC / "json_mini.h", CSRC / "safetensors_mini.h", PKG.parent / "include" / "dcamd.h"]
 
 
 def source_hash() -> str:
@@ -46,7 +46,7 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
 
 def build(verbose: bool = False, force: bool = False) -> Path:
     OBJ_DIR.mkdir(exist_ok=True)
-    headers = [CSRC / "common.h", CSRC / "json_mini.h", PKG.parent / "include" / "dcamd.h"]
+    headers = [CSRC / "common.h", CSRC / "json_mini.h", CSRC / "safetensors_mini.h", PKG.parent / "include" / "dcamd.h"]
     bid = source_hash()
     jobs = []
     for src in SOURCES:

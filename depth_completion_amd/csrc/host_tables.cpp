@@ -29,7 +29,7 @@ inline float round_bf16(float f) {
 extern "C" int dc_schedule_tables(int steps, double lr_latent, double lr_scaling, int opt, long long* timesteps,
                                   float* coef, float* adam) {
   constexpr int T = 1000;
-  if (steps <= 0 || steps > T || opt < 0 || opt > 2) return 1;
+  if (steps <= 0 || steps > T || opt < 0 || opt > 2 || !timesteps || !coef || !adam) return 1;
   // betas = linspace(sqrt(0.00085), sqrt(0.012), T, fp32) ** 2; alphas_cumprod = cumprod(1 - betas)
   // (torch's linspace: start + step * i below the midpoint, end - step * (T - 1 - i) above; cumprod
   // accumulates in double and stores fp32)
@@ -104,7 +104,8 @@ extern "C" int dc_fold_cross_attention(const float* wq, const float* wk, const f
   // softmax over the 2 context tokens: p0 = sigmoid(q . (k0 - k1) / sqrt(hd)); out = v1 + p0 (v0 - v1) per head:
   //   U_h = Wq_h^T (k0_h - k1_h) / sqrt(hd),  D_h = Wo_h (v0_h - v1_h),  c0 = Wo v1 + bo
   // in double from bf16-rounded weights; k, v rounded to bf16 as the reference's to_k / to_v produce them
-  if (ntok != 2 || heads <= 0 || inner % heads || !wq || !wk || !wv || !wo || !bo || !ctx) return 1;
+  if (ntok != 2 || heads <= 0 || inner <= 0 || inner % heads || c <= 0 || cross <= 0 || cout <= 0) return 1;
+  if (!wq || !wk || !wv || !wo || !bo || !ctx || !U || !D || !c0) return 1;
   const int hd = inner / heads;
   std::vector<double> k(2 * (size_t)inner), v(2 * (size_t)inner);
   for (int t = 0; t < 2; ++t)

@@ -34,6 +34,8 @@ struct Value {
   long long as_int() const {
     if (kind == Bool) return b ? 1 : 0;
     if (kind != Num) throw std::runtime_error("json: not a number");
+    // |v| < 2^62: the conversion is defined, and sizes / offsets built from it cannot overflow a product
+    if (!(num > -4.6e18 && num < 4.6e18)) throw std::runtime_error("json: integer out of range");
     return (long long)num;
   }
   double as_num() const {
@@ -55,6 +57,8 @@ class Parser {
  private:
   const char* s_;
   size_t n_, i_ = 0;
+  int depth_ = 0;
+  static constexpr int kMaxDepth = 128;  // nesting bound: a hostile header cannot exhaust the stack
   [[noreturn]] void fail(const char* what) {
     throw std::runtime_error(std::string("json: ") + what + " at byte " + std::to_string(i_));
   }
@@ -71,7 +75,7 @@ class Parser {
     return true;
   }
   std::string string_() {
-    if (s_[i_] != '"') fail("expected string");
+    if (i_ >= n_ || s_[i_] != '"') fail("expected string");
     ++i_;
     std::string out;
     while (i_ < n_ && s_[i_] != '"') {
@@ -114,6 +118,11 @@ class Parser {
   Value value() {
     ws();
     if (i_ >= n_) fail("unexpected end");
+    if (++depth_ > kMaxDepth) fail("nesting too deep");
+    struct Leave {
+      int& d;
+      ~Leave() { --d; }
+    } leave{depth_};
     Value v;
     char c = s_[i_];
     if (c == '{') {

@@ -36,6 +36,7 @@
 
 #include "../../include/dcamd.h"
 #include "json_mini.h"
+#include "safetensors_mini.h"
 
 namespace {
 
@@ -65,86 +66,11 @@ inline uint16_t f2bf(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
-inline float bf2f(uint16_t h) {
-  const uint32_t u = (uint32_t)h << 16;
-  float f;
-  memcpy(&f, &u, 4);
-  return f;
-}
-inline float round_bf16(float f) { return bf2f(f2bf(f)); }
-inline float half2f(uint16_t h) {
-  const uint32_t s = (h >> 15) & 1u, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
-  float v;
-  if (e == 0) v = std::ldexp((float)m, -24);
-  else if (e == 31) v = m ? NAN : INFINITY;
-  else v = std::ldexp((float)(m | 0x400u), (int)e - 25);
-  return s ? -v : v;
-}
-
-// ------------------------------------------------------------------ safetensors (read-only mmap)
-struct HostTensor {
-  std::vector<long> shape;
-  std::vector<float> data;  // converted to fp32
-  long numel() const {
-    long n = 1;
-    for (long s : shape) n *= s;
-    return n;
-  }
-};
-
-class SafeTensors {
- public:
-  explicit SafeTensors(const std::string& path) : path_(path) {
-    fd_ = open(path.c_str(), O_RDONLY);
-    if (fd_ < 0) throw DcError(kErrArg, "cannot open " + path);
-    struct stat st;
-    fstat(fd_, &st);
-    size_ = (size_t)st.st_size;
-    base_ = (const char*)mmap(nullptr, size_, PROT_READ, MAP_PRIVATE, fd_, 0);
-    if (base_ == MAP_FAILED || size_ < 8) throw DcError(kErrArg, "cannot map " + path);
-    uint64_t hl;
-    memcpy(&hl, base_, 8);
-    if (8 + hl > size_) throw DcError(kErrArg, "bad safetensors header in " + path);
-    head_ = dcjson::parse(std::string(base_ + 8, hl));
-    data_ = base_ + 8 + hl;
-  }
-  ~SafeTensors() {
-    if (base_ && base_ != MAP_FAILED) munmap((void*)base_, size_);
-    if (fd_ >= 0) close(fd_);
-  }
-  bool has(const std::string& k) const { return head_.get(k) != nullptr; }
-  HostTensor get(const std::string& k) const {
-    const dcjson::Value* v = head_.get(k);
-    if (!v) throw DcError(kErrArg, "missing tensor '" + k + "' in " + path_);
-    HostTensor t;
-    for (auto& s : v->at("shape").arr) t.shape.push_back((long)s.as_int());
-    const std::string dt = v->at("dtype").str;
-    const auto& off = v->at("data_offsets").arr;
-    const char* p = data_ + off.at(0).as_int();
-    const long n = t.numel();
-    t.data.resize((size_t)n);
-    if (dt == "F32") {
-      memcpy(t.data.data(), p, (size_t)n * 4);
-    } else if (dt == "BF16") {
-      for (long i = 0; i < n; ++i) { uint16_t h; memcpy(&h, p + 2 * i, 2); t.data[i] = bf2f(h); }
-    } else if (dt == "F16") {
-      for (long i = 0; i < n; ++i) { uint16_t h; memcpy(&h, p + 2 * i, 2); t.data[i] = half2f(h); }
-    } else if (dt == "F64") {
-      for (long i = 0; i < n; ++i) { double d; memcpy(&d, p + 8 * i, 8); t.data[i] = (float)d; }
-    } else {
-      throw DcError(kErrArg, "unsupported dtype " + dt + " for " + k);
-    }
-    return t;
-  }
-
- private:
-  std::string path_;
-  int fd_ = -1;
-  size_t size_ = 0;
-  const char* base_ = nullptr;
-  const char* data_ = nullptr;
-  dcjson::Value head_;
-};
+inline float round_bf16(float f) { return dcst::bf2f(f2bf(f)); }
+// ------------------------------------------------------------------ safetensors (read-only mmap, validated)
+using dcst::bf2f;
+using dcst::HostTensor;
+using dcst::SafeTensors;
 
 std::string read_file(const std::string& path) {
   FILE* f = fopen(path.c_str(), "rb");
