@@ -103,6 +103,30 @@ def discover(src_root: Path, use_segmask: bool):
     return plan
 
 
+def frame_outputs(out_dir: Path, img_dir: Path, sp_dir: Path, ip: Path, sp: Path, compress: str, save_dense: bool,
+                  vis: bool) -> list:
+    """The files one input pair writes (dense map and/or visualisation), as the loop below names them."""
+    outs = []
+    if save_dense:
+        outs.append((out_dir / dio.RESULT_DIR_NAME_DENSE / sp.relative_to(sp_dir)).parent
+                    / sp.with_suffix(f".{compress}").name)
+    if vis:
+        outs.append((out_dir / dio.RESULT_DIR_NAME_VIS / ip.relative_to(img_dir)).parent / f"{ip.stem}_vis.jpg")
+    return outs
+
+
+def pending_pairs(pairs: list, out_dir: Path, img_dir: Path, sp_dir: Path, compress: str, save_dense: bool,
+                  vis: bool) -> list:
+    """--resume: drop the pairs whose every output already exists (SURVEY.md §5 'checkpoint / resume'; the
+    reference has none and re-runs overwrite).  A pair with any output missing is re-run in full."""
+    keep = []
+    for ip, sp, sm in pairs:
+        outs = frame_outputs(out_dir, img_dir, sp_dir, ip, sp, compress, save_dense, vis)
+        if not outs or not all(o.exists() for o in outs):
+            keep.append((ip, sp, sm))
+    return keep
+
+
 @click.command(help="Predict dense depth maps from sparse depth maps and camera images (MI355X).")
 @click.argument("src_root", type=click.Path(exists=True, path_type=Path, file_okay=False, dir_okay=True))
 @click.argument("dst_root", type=click.Path(exists=False, path_type=Path))
@@ -150,11 +174,13 @@ def discover(src_root: Path, use_segmask: bool):
 @click.option("--synthetic-weights", type=int, default=None, help="Seeded synthetic weights (no checkpoint).")
 @click.option("--unet-config", type=click.Choice(["marigold-v1", "tiny"]), default="marigold-v1", hidden=True)
 @click.option("--dry-run", is_flag=True, help="Discover and list the input pairs, run nothing.")
+@click.option("--resume", is_flag=True, help="Skip input pairs whose outputs already exist (default: overwrite, as "
+              "the reference does). With --use-prev-latent the warm-start chain restarts at the first pending frame.")
 def main(src_root, dst_root, model, vae, steps, res, norm, percentile, max_sparse_depth, max_depth, min_depth, vis,
          vis_res, vis_order, save_dense, log, log_level, precision, compress, compile_graph, compile_mode,
          interp_mode, loss_funcs, opt, lr_latent, lr_scaling, kld, kld_mode, kld_weight, batch_size,
          use_prev_latent, beta, use_segmask, closed_form, projection, inv, train_latents, train_method, train_steps,
-         weights, synthetic_weights, unet_config, dry_run):
+         weights, synthetic_weights, unet_config, dry_run, resume):
     level = {"TRACE": "DEBUG", "SUCCESS": "INFO"}.get(log_level, log_level)
     logging.basicConfig(level=getattr(logging, level), format="%(asctime)s %(levelname)s %(message)s",
                         stream=sys.stderr)
@@ -242,6 +268,10 @@ def main(src_root, dst_root, model, vae, steps, res, norm, percentile, max_spars
         out_dir = dst_root / d.relative_to(src_root)
         img_dir, sp_dir = d / dio.DATASET_DIR_NAME_IMAGE, d / dio.DATASET_DIR_NAME_SPARSE
         mine = [pairs[i] for i in frame_shard(len(pairs), rank, world)]
+        if resume:
+            n_all = len(mine)
+            mine = pending_pairs(mine, out_dir, img_dir, sp_dir, compress, save_dense, vis)
+            logger.info(f"--resume: {n_all - len(mine)} of {n_all} frames already done on rank {rank}")
         prev = None
         t0 = time.time()
         for b in range(0, len(mine), batch_size):
@@ -267,9 +297,9 @@ def main(src_root, dst_root, model, vae, steps, res, norm, percentile, max_spars
                 if dio.has_nan(dense):
                     logger.error("NaN values found in dense depth map (skipped)")
                     continue
+                outs = frame_outputs(out_dir, img_dir, sp_dir, ip, sp, compress, save_dense, vis)
                 if save_dense:
-                    save_dir = (out_dir / dio.RESULT_DIR_NAME_DENSE / sp.relative_to(sp_dir)).parent
-                    dio.save_tensor(dense, save_dir / sp.with_suffix(f".{compress}").name, compress=compress)
+                    dio.save_tensor(dense, outs[0], compress=compress)
                 if vis:
                     mask = (sparse <= 0.0).repeat(img.shape[0], 1, 1).cpu()
                     views = []
@@ -284,8 +314,7 @@ def main(src_root, dst_root, model, vae, steps, res, norm, percentile, max_spars
                             views.append(dio.visualize_depth(dense[None].cpu(), max_depth=max_depth,
                                                              min_depth=min_depth)[0])
                     grid = dio.make_grid(views, resize=tuple(vis_res))
-                    save_dir = (out_dir / dio.RESULT_DIR_NAME_VIS / ip.relative_to(img_dir)).parent
-                    dio.save_img_tensor(grid, save_dir / f"{ip.stem}_vis.jpg")
+                    dio.save_img_tensor(grid, outs[-1])
         logger.info(f"Finished processing {d.name} (rank {rank}/{world}: {len(mine)} frames, {time.time() - t0:.1f}s)")
     logger.info(f"Finished processing all {len(plan):,} datasets")
 

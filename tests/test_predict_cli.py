@@ -97,3 +97,21 @@ def test_cli_dry_run_and_coercions(tmp_path):
     assert r.exit_code != 0
     r = CliRunner().invoke(main, [str(tmp_path), str(tmp_path / "out2"), "--dry-run", "--steps", "0"])
     assert r.exit_code != 0  # IntRange(min=1)
+
+
+def test_resume_pending_pairs(tmp_path):
+    """--resume drops the pairs whose every output exists; a pair with one output missing is re-run."""
+    from depth_completion_amd.predict import discover, frame_outputs, pending_pairs
+    root = make_dataset(tmp_path / "data", n=3)
+    (d, pairs, _), = discover(root, False)
+    img_dir, sp_dir, out = d / "image", d / "sparse", tmp_path / "out"
+    assert pending_pairs(pairs, out, img_dir, sp_dir, "npy", True, True) == pairs
+    done = frame_outputs(out, img_dir, sp_dir, *pairs[0][:2], "npy", True, True)
+    half = frame_outputs(out, img_dir, sp_dir, *pairs[1][:2], "npy", True, True)
+    assert done[0].name == "0000.npy" and done[1].name == "0000_vis.jpg"
+    for p in done + half[:1]:
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_bytes(b"x")
+    assert pending_pairs(pairs, out, img_dir, sp_dir, "npy", True, True) == pairs[1:]
+    assert pending_pairs(pairs, out, img_dir, sp_dir, "npy", True, False) == pairs[2:]   # vis off: dense suffices
+    assert pending_pairs(pairs, out, img_dir, sp_dir, "npz", True, False) == pairs        # other format: pending
