@@ -375,19 +375,11 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
   for (int s = 0; s < 4; ++s) qf[s] = load_row8(base + (long)my_q * ld + h * 64 + 16 * s + 8 * hh, qok, 0.125f);
 
   float m = -INFINITY, l = 0.0f;
-  f32x16 oacc[2], lacc;
+  f32x16 oacc[2];
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[db][r] = 0.0f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) lacc[r] = 0.0f;
-  // row sums on the MFMA pipe (the softmax is VALU-issue bound, the MFMAs are not): a ones A-operand
-  // against the P fragment gives sum_k P[q][k] in every element of lane q's accumulator, summed from
-  // the same bf16 P the P.V product uses
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
 
   const int per = (tcount + KS - 1) / KS;
   const int tb = t0 + part * per;
@@ -465,15 +457,23 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
         for (int db = 0; db < 2; ++db)
 #pragma unroll
           for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) lacc[r] *= alpha;
+        l *= alpha;
         m = mnew;
       }
+      // row sums in fp32 from the unrounded weights: the LSE the backward recomputes P from must not carry
+      // P's bf16 rounding (a sum of bf16 P, e.g. on the MFMA pipe, is off by up to ~4e-3 in the LSE on
+      // peaked rows and biases the guidance gradient: tools/attn_acc.py, profiles/r02m)
       const float ml = m * LOG2E;
+      float ps = 0.0f;
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[b][r] = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+          sacc[b][r] = pv;
+          ps += pv;
+        }
+      l += ps;
       // V^T fragments: two k-slices in flight ahead of the MFMAs that consume them
       constexpr int VIMM = ST * FwdLds<QW, KS>::STAGE + TILE_B;
       bf16x8 vf[4][2];
@@ -496,7 +496,6 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
 #pragma unroll
         for (int db = 0; db < 2; ++db)
           oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], pf, oacc[db], 0, 0, 0);
-        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf, lacc, 0, 0, 0);
       }
     }
   };
@@ -508,7 +507,7 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
   }
   vm_wait_n<0>();
   __syncthreads();
-  l = lacc[0];  // the full row sum (both lane halves of the row hold it)
+  l += __shfl_xor(l, 32, 64);  // the two lane halves of a row hold the sums of alternate key groups
   if constexpr (KS > 1) {
     // merge the key-split partials: parts 1.. publish (m, l, O) per lane, part 0 folds them in order
     float* red = reinterpret_cast<float*>(smem);
@@ -594,27 +593,6 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 }
 
 // ------------------------------------------------------------------------------ backward
-// delta[n][h][q] = sum_d dO * O  (fp32)
-__global__ void attn_delta_kernel(const bf16* o, int ldo, const bf16* dout, int lddo, int T, int heads, long total,
-                                  float* delta) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total) return;
-  const int h = (int)(idx % heads);
-  const long nq = idx / heads;  // n*T + q
-  const int q = (int)(nq % T);
-  const long n = nq / T;
-  float s = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float a[8], b[8];
-    load8(o + nq * ldo + h * 64 + 8 * k, a);
-    load8(dout + nq * lddo + h * 64 + 8 * k, b);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s += a[i] * b[i];
-  }
-  delta[(n * heads + h) * T + q] = s;
-}
-
 // dK/dV: 32 QW keys per block resident in registers (32 per wave); KS query-splits per block (waves
 // QW p .. QW p + QW - 1 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a
 // fixed order.  Q / dO tiles (+ lse / delta rows) stream through an LDS-DMA ring; Q is not pre-scaled
@@ -879,10 +857,10 @@ struct DqLds {
 };
 
 template <int QW, int KS, bool SK>
-__device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, const bf16* dout, int lddo,
-                                           const float* lse, const float* delta, int T, int heads, bf16* dqkv,
-                                           int ldd, int qbk, int h, int n, int t0, int tcount, const AttnSK& sk,
-                                           long bi, int seg) {
+__device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, const bf16* o, int ldo,
+                                           const bf16* dout, int lddo, const float* lse, float* delta, int T,
+                                           int heads, bf16* dqkv, int ldd, int qbk, int h, int n, int t0, int tcount,
+                                           const AttnSK& sk, long bi, int seg) {
   constexpr int NT = 64 * QW;
   constexpr int S = BWD_S;
   constexpr int STG = DqLds<QW, KS>::STAGE;
@@ -901,7 +879,18 @@ __device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, 
     df[s] = load_row8(dout + ((long)n * T + my_q) * lddo + h * 64 + 16 * s + 8 * hh, qok, 1.0f);
   }
   const float my_lse = qok ? lse[((long)n * heads + h) * T + my_q] * LOG2E : INFINITY;
-  const float my_del = qok ? delta[((long)n * heads + h) * T + my_q] : 0.0f;
+  // delta = sum_d dO * O of this lane's query, from the dO fragments already in registers and the same
+  // pieces of O (fp32, fixed order); the key-range segment that starts the row (t0 = 0, part 0) publishes it
+  // for the dK/dV kernel, which runs after this one
+  float my_del = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const bf16x8 of = load_row8(o + ((long)n * T + my_q) * ldo + h * 64 + 16 * s + 8 * hh, qok, 1.0f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) my_del = fmaf((float)df[s][j], (float)of[j], my_del);
+  }
+  my_del += __shfl_xor(my_del, 32, 64);
+  if (qok && hh == 0 && part == 0 && t0 == 0) delta[((long)n * heads + h) * T + my_q] = my_del;
   f32x16 dq[2];
 #pragma unroll
   for (int db = 0; db < 2; ++db)
@@ -1045,20 +1034,20 @@ __device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, 
 
 template <int QW, int KS, bool SK>
 __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(
-    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
-    bf16* dqkv, int ldd, AttnSK sk) {
+    const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse, float* delta,
+    int T, int heads, bf16* dqkv, int ldd, AttnSK sk) {
   __shared__ __attribute__((aligned(16))) char smem[DqLds<QW, KS>::BYTES];
   const int ntk = (T + 63) / 64;
   if constexpr (!SK) {
-    dq_segment<QW, KS, false>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, blockIdx.x, blockIdx.y,
-                              blockIdx.z, 0, ntk, sk, 0, 0);
+    dq_segment<QW, KS, false>(smem, qkv, ld, o, ldo, dout, lddo, lse, delta, T, heads, dqkv, ldd, blockIdx.x,
+                              blockIdx.y, blockIdx.z, 0, ntk, sk, 0, 0);
   } else {
     const int nqb = (T + 32 * QW - 1) / (32 * QW);
     sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
       const int qbk = (int)(bi % nqb);
       const long nh = bi / nqb;
-      dq_segment<QW, KS, true>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, qbk, (int)(nh % heads),
-                               (int)(nh / heads), t0, cnt, sk, bi, seg);
+      dq_segment<QW, KS, true>(smem, qkv, ld, o, ldo, dout, lddo, lse, delta, T, heads, dqkv, ldd, qbk,
+                               (int)(nh % heads), (int)(nh / heads), t0, cnt, sk, bi, seg);
     });
   }
 }
@@ -1107,14 +1096,16 @@ void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int 
                      none);
 }
 
+// dQ first: it computes delta = rowsum(dO * O) for its resident queries and publishes it; dK/dV (next
+// launch, same stream) reads it -- no separate delta pass
 template <int QW, int KS>
-void launch_bwd(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
-                int heads, int nb, bf16* dqkv, int ldd, hipStream_t st) {
+void launch_bwd(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
+                float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
   const AttnSK none{};
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, o, ldo, dout, lddo,
+                     lse, delta, t, heads, dqkv, ldd, none);
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse,
-                     delta, t, heads, dqkv, ldd, none);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse,
                      delta, t, heads, dqkv, ldd, none);
 }
 
@@ -1156,13 +1147,14 @@ bool sk_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env
   return true;
 }
 
-bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
-                   int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
+bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
+                   float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes,
+                   hipStream_t st) {
   AttnSK sk;
   if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK", sk)) return false;
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, o, ldo, dout,
+                     lddo, lse, delta, t, heads, dqkv, ldd, sk);
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout, lddo,
-                     lse, delta, t, heads, dqkv, ldd, sk);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout, lddo,
                      lse, delta, t, heads, dqkv, ldd, sk);
   return true;
 }
@@ -1209,21 +1201,19 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   if (!qkv || !o || !dout || !lse || !delta_ws || !dqkv || nb <= 0 || t <= 0 || heads <= 0) return DC_ERR_ARG;
   if (ld % 8 || ldo % 8 || lddo % 8 || ldd % 8 || ldd < 3 * heads * 64) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
-  const long total = (long)nb * t * heads;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, (const bf16*)o, ldo,
-                     (const bf16*)dout, lddo, t, heads, total, delta_ws);
   const bf16* q = (const bf16*)qkv;
+  const bf16* ob = (const bf16*)o;
   const bf16* d = (const bf16*)dout;
   bf16* g = (bf16*)dqkv;
-  if (launch_bwd_sk(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0,
-                    st)) {
+  if (launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws,
+                    ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st)) {
     DC_CHECK_LAUNCH();
     return DC_OK;
   }
   switch (attn_cfg(t, heads, nb, true)) {
-    case 0: launch_bwd<4, 1>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
-    case 1: launch_bwd<4, 2>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
-    default: launch_bwd<2, 2>(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
+    case 0: launch_bwd<4, 1>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
+    case 1: launch_bwd<4, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
+    default: launch_bwd<2, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
   }
   DC_CHECK_LAUNCH();
   return DC_OK;
