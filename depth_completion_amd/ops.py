@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
+import sys
 from dataclasses import dataclass
 from pathlib import Path
 
@@ -201,6 +202,8 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3) -> tuple:
             t = e0.elapsed_time(e1)
         if t < best_t * 0.97:  # prefer the earlier (heuristic / fewer splits) on near-ties
             best, best_t = (a, s), t
+    print(f"tuned {conv_key(d)} -> {best} ({best_t / reps * 1e3:.1f} us)", file=sys.stderr,
+          flush=True)
     return best
 
 

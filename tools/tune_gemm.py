@@ -5,7 +5,9 @@ The committed table is tuned with DC_TUNE_COLD=1 (caches flushed before every ti
 Runs one eager guided call per workload with Ctx.tune on (each new shape is timed over all tile
 algos x split-K on its real operands) and writes the table that ops.load_tuned() reads.
 
-Usage: python tools/tune_gemm.py [--batches 1 8] [--out depth_completion_amd/tuned_gfx950.json]
+Usage: python tools/tune_gemm.py [--workloads c2:1 c2:8 c4:1 c4:8 c5:1] [--out depth_completion_amd/tuned_gfx950.json]
+  workload:batch -- c2 / c3: 768x576, 500 uniform points; c4: 1216x352, 64-beam rows; c5: 1600x900, 3000
+  points, run as the 10-seed ensemble (one batch-10 call per frame, the shapes C5 launches)
 """
 import argparse
 import os
@@ -22,7 +24,7 @@ from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline  # noq
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batches", type=int, nargs="+", default=[1, 8])
+    ap.add_argument("--workloads", nargs="+", default=["c2:1", "c2:8"])
     ap.add_argument("--out", default="gpurun_out/tuned_gfx950.json")
     ap.add_argument("--fresh", action="store_true", help="ignore the committed table")
     args = ap.parse_args()
@@ -32,14 +34,22 @@ def main():
     if args.fresh:
         pipe.ctx.algo_cache = {}
     pipe.ctx.tune = True
-    for b in args.batches:
-        fr = [synth_frame(576, 768, 500, i) for i in range(b)]
+    shapes = {"c2": (576, 768, 500, "uniform"), "c3": (576, 768, 500, "uniform"), "c4": (352, 1216, 0, "beams"),
+              "c5": (900, 1600, 3000, "uniform")}
+    for wl in args.workloads:
+        name, b = wl.split(":")
+        h, w, npts, pattern = shapes[name]
+        fr = [synth_frame(h, w, npts, i, pattern) for i in range(int(b))]
         imgs = torch.stack([f[0] for f in fr]).to(dev)
         sps = torch.stack([f[1] for f in fr]).to(dev)
         n0 = len(pipe.ctx.algo_cache)
-        pipe(imgs, sps, 120.0, norm="const", steps=2, resolution=768)
+        if name == "c5":
+            pipe.ensemble(imgs, sps, 120.0, seeds=list(range(2024, 2034)), norm="const", steps=2, resolution=768)
+        else:
+            pipe(imgs, sps, 120.0, norm="const", steps=2, resolution=768)
         torch.cuda.synchronize()
-        print(f"batch {b}: {len(pipe.ctx.algo_cache) - n0} new shapes tuned", flush=True)
+        print(f"{wl}: {len(pipe.ctx.algo_cache) - n0} new shapes tuned", flush=True)
+        ops.save_tuned(pipe.ctx.algo_cache, args.out)   # keep what is done if a later workload is cut off
     ops.save_tuned(pipe.ctx.algo_cache, args.out)
     for k, v in sorted(pipe.ctx.algo_cache.items()):
         print(k, v)
