@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -104,6 +104,7 @@ _SIGS.update({
     "dc_schedule_tables": [i32, C.c_double, C.c_double, i32, vp, vp, vp],
     "dc_timestep_embedding": [vp, i32, i32, vp],
     "dc_fold_cross_attention": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+    "dc_conv_pick": [vp, vp, i32, vp, vp],
     "dc_sample_params_default": [vp],
     "dc_latent_hw": [i32, i32, i32, vp, vp],
     "dc_create": [vp, i32],

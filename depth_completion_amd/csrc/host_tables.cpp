@@ -6,6 +6,7 @@
 //                            reduced to per-step scalars, and torch.optim.Adam's bias corrections (:783, 897)
 //   dc_timestep_embedding    diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), fp32
 //   dc_fold_cross_attention  attn2 with the constant 2-token empty-prompt context folded to (U, D, c0)
+//   dc_conv_pick             the tuned GEMM variant of a conv shape, nearest tuned shape for shapes not in the table
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -139,5 +140,35 @@ extern "C" int dc_fold_cross_attention(const float* wq, const float* wk, const f
     for (int j = 0; j < inner; ++j) s += (double)round_bf16(wo[(size_t)o * inner + j]) * v[(size_t)inner + j];
     c0[o] = (float)(s + (double)round_bf16(bo[o]));
   }
+  return 0;
+}
+
+extern "C" int dc_conv_pick(const int* keys, const int* choices, int n, const int* key, int* out) {
+  if (!out) return 1;
+  out[0] = 0;
+  out[1] = 0;
+  if (!keys || !choices || !key || n <= 0) return 1;
+  auto lg = [](long long v) { return std::log2((double)(v > 0 ? v : 1)); };
+  const long long m = (long long)key[1] * key[5] * key[6];
+  const double lm = lg(m), ln = lg(key[7]), lk = lg(key[11]);
+  int best = -1;
+  double best_d = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const int* k = keys + 12 * (long)i;
+    if (std::memcmp(k, key, 12 * sizeof(int)) == 0) {
+      best = i;
+      break;
+    }
+    if (k[0] != key[0] || k[8] != key[8] || k[9] != key[9] || k[10] != key[10]) continue;
+    const double d = 4.0 * std::fabs(lg((long long)k[1] * k[5] * k[6]) - lm) + std::fabs(lg(k[7]) - ln) +
+                     std::fabs(lg(k[11]) - lk);
+    if (best < 0 || d < best_d) {
+      best = i;
+      best_d = d;
+    }
+  }
+  if (best < 0) return 1;
+  out[0] = choices[2 * best];
+  out[1] = choices[2 * best + 1];
   return 0;
 }

@@ -247,6 +247,11 @@ struct Exec {
   long long ws_bytes = 0;
   int* step = nullptr;  // device step counter
   std::map<ConvKey, std::pair<int, int>> tuned;
+  // the tuned table in file order (dc_conv_pick picks the nearest tuned shape for a shape not in it, as the
+  // Python host's ops.Ctx does), and the picks made so far
+  std::vector<int> table_keys, table_choices;
+  std::map<ConvKey, std::pair<int, int>> picked;
+  bool nn = true;
 
   // ops.conv_gemm
   struct Conv {
@@ -307,8 +312,19 @@ struct Exec {
     } else {
       const ConvKey key{d.mode, d.nb, d.hin, d.win, d.cin, d.hout, d.wout, d.cout, d.kh, d.stride, d.x2 ? 1 : 0, d.ktot};
       auto it = tuned.find(key);
-      d.algo = it == tuned.end() ? 0 : it->second.first;
-      d.splitk = it == tuned.end() ? 0 : it->second.second;
+      if (it == tuned.end()) {
+        it = picked.find(key);
+        if (it == picked.end()) {
+          int out[2] = {0, 0};
+          const int kk[12] = {d.mode, d.nb, d.hin, d.win, d.cin, d.hout, d.wout, d.cout, d.kh, d.stride, d.x2 ? 1 : 0,
+                              d.ktot};
+          if (nn && !table_choices.empty())
+            (void)dc_conv_pick(table_keys.data(), table_choices.data(), (int)(table_choices.size() / 2), kk, out);
+          it = picked.emplace(key, std::make_pair(out[0], out[1])).first;
+        }
+      }
+      d.algo = it->second.first;
+      d.splitk = it->second.second;
     }
     DCK(dc_conv_gemm(&d, stream));
   }
@@ -349,13 +365,26 @@ void load_tuned(Exec& ex, const std::string& path) {
   const std::string s = read_file(path);
   if (s.empty()) return;
   dcjson::Value v = dcjson::parse(s);
+  std::map<ConvKey, int> index;
   for (const auto& e : v.arr) {
     const auto& k = e.at("key").arr;
     if (k.size() != 12) continue;
     ConvKey key{(int)k[0].as_int(), (int)k[1].as_int(), (int)k[2].as_int(), (int)k[3].as_int(), (int)k[4].as_int(),
                 (int)k[5].as_int(), (int)k[6].as_int(), (int)k[7].as_int(), (int)k[8].as_int(), (int)k[9].as_int(),
                 (int)k[10].as_int(), (int)k[11].as_int()};
-    ex.tuned[key] = {(int)e.at("algo").as_int(), (int)e.at("splitk").as_int()};
+    const int algo = (int)e.at("algo").as_int(), splitk = (int)e.at("splitk").as_int();
+    // a repeated key keeps its first position and takes the last value, as the Python host's dict does
+    auto pos = index.find(key);
+    if (pos != index.end()) {
+      ex.table_choices[2 * pos->second] = algo;
+      ex.table_choices[2 * pos->second + 1] = splitk;
+    } else {
+      index[key] = (int)(ex.table_choices.size() / 2);
+      for (const auto& kv : k) ex.table_keys.push_back((int)kv.as_int());
+      ex.table_choices.push_back(algo);
+      ex.table_choices.push_back(splitk);
+    }
+    ex.tuned[key] = {algo, splitk};
   }
 }
 
@@ -1646,6 +1675,11 @@ extern "C" int dc_load_weights(dc_session* s, const char* dir, const char* tuned
       load_taesd(s->taesd, L);
     }
     s->ex.tuned.clear();
+    s->ex.table_keys.clear();
+    s->ex.table_choices.clear();
+    s->ex.picked.clear();
+    const char* nn = getenv("DC_GEMM_NN");
+    s->ex.nn = !(nn && std::string(nn) == "0");
     if (tuned_table && *tuned_table) load_tuned(s->ex, tuned_table);
     s->loaded = true;
     s->err.clear();

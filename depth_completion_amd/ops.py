@@ -85,14 +85,23 @@ class Ctx:
         self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.algo_cache: dict = load_tuned()
         self.tune = os.environ.get("DC_TUNE") == "1" if tune is None else tune
+        # the committed table in file order, for dc_conv_pick's nearest-shape choice (the native session passes
+        # the same table in the same order, so both hosts launch the same variants)
+        self._table = list(self.algo_cache.items())
+        self._picked: dict = {}
 
     def choose_algo(self, d, y=None):
-        """(algo, splitk) for a conv descriptor: tuned table / autotune, else the library heuristic."""
+        """(algo, splitk) for a conv descriptor: tuned table / autotune; a shape missing from the table takes
+        the variant of the nearest tuned shape (dc_conv_pick; DC_GEMM_NN=0: the library heuristic instead)."""
         key = conv_key(d)
         if key not in self.algo_cache and self.tune and self.device.type == "cuda" \
                 and not torch.cuda.is_current_stream_capturing():
             self.algo_cache[key] = _autotune(self, d, y)
-        return self.algo_cache.get(key, (0, 0))
+        if key in self.algo_cache:
+            return self.algo_cache[key]
+        if key not in self._picked:
+            self._picked[key] = pick_variant(self._table, key)
+        return self._picked[key]
 
     @property
     def stream(self) -> int:
@@ -108,6 +117,18 @@ class Ctx:
 # ------------------------------------------------------------------------- conv / linear
 def conv_key(d) -> tuple:
     return (d.mode, d.nb, d.hin, d.win, d.cin, d.hout, d.wout, d.cout, d.kh, d.stride, bool(d.x2), d.ktot)
+
+
+def pick_variant(table: list, key: tuple) -> tuple:
+    """dc_conv_pick over ``table`` [(key, (algo, splitk))] in order: exact match, else the nearest tuned shape."""
+    if not table or os.environ.get("DC_GEMM_NN") == "0":
+        return (0, 0)
+    keys = (C.c_int * (12 * len(table)))(*[int(v) for k, _ in table for v in k])
+    choices = (C.c_int * (2 * len(table)))(*[int(v) for _, c in table for v in c])
+    kk = (C.c_int * 12)(*[int(v) for v in key])
+    out = (C.c_int * 2)()
+    _lib.load().dc_conv_pick(C.addressof(keys), C.addressof(choices), len(table), C.addressof(kk), C.addressof(out))
+    return (out[0], out[1])
 
 
 def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin: int, hout: int, wout: int,

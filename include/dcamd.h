@@ -290,6 +290,14 @@ int dc_timestep_embedding(const long long* timesteps, int n, int dim, float* out
 int dc_fold_cross_attention(const float* wq, const float* wk, const float* wv, const float* wo, const float* bo,
                             const float* ctx, int ntok, int inner, int c, int cross, int cout, int heads, float* U,
                             float* D, float* c0);
+/* dc_conv_pick: the dc_conv_gemm variant for a conv shape from a tuned table (tools/tune_gemm.py; both hosts call
+ * it, so they launch the same variant).  keys[n][12] = (mode, nb, hin, win, cin, hout, wout, cout, kh, stride,
+ * two_sources, ktot) in table order, choices[n][2] = (algo, splitk), key[12] the shape.  An exact match wins;
+ * otherwise the nearest tuned shape with the same (mode, kh, stride, two_sources) in
+ * 4 |log2 M - log2 M'| + |log2 N - log2 N'| + |log2 K - log2 K'| (M = nb hout wout, N = cout, K = ktot; first
+ * in table order on ties).  out[2] = (algo, splitk); returns 0, or 1 when no entry qualifies (out = (0, 0): the
+ * library heuristic). */
+int dc_conv_pick(const int* keys, const int* choices, int n, const int* key, int* out);
 
 /* ---------------------------------------------------------------- native session
  * The whole guided sampler behind an opaque handle, for hosts that are not Python: the same weight packing,

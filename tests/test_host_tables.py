@@ -139,3 +139,26 @@ def test_text_embedding_computed_from_text_encoder(tmp_path):
     assert emb.shape == (1, 2, 64) and torch.isfinite(emb).all()
     assert (d / "empty_text_embedding.safetensors").exists()   # cached for the native session
     assert torch.equal(pt.empty_text_embedding(d), emb)
+
+
+def test_conv_pick_exact_nearest_and_filters():
+    """dc_conv_pick (both hosts' GEMM variant choice): exact key first; else the nearest tuned shape with the same
+    (mode, kh, stride, two_sources) in 4|dlog2 M| + |dlog2 N| + |dlog2 K|, first in table order on ties."""
+    from depth_completion_amd.ops import pick_variant
+    base = (0, 1, 72, 96, 320, 72, 96, 320, 3, 1, False, 2880)      # M 6912, N 320, K 2880
+    table = [(base, (13, -3)),
+             ((0, 1, 18, 24, 1280, 18, 24, 1280, 3, 1, False, 11520), (3, 2)),   # M 432
+             ((0, 1, 1, 6912, 320, 1, 6912, 320, 1, 1, False, 320), (18, 4)),    # 1x1, other kh
+             ((0, 1, 72, 96, 640, 72, 96, 320, 3, 1, True, 5760), (10, 1)),     # two sources
+             ((0, 8, 72, 96, 320, 72, 96, 320, 3, 1, False, 2880), (6, 1))]     # M 55296
+    assert pick_variant(table, base) == (13, -3)
+    assert pick_variant(table, (0, 1, 28, 96, 320, 28, 96, 320, 3, 1, False, 2880)) == (13, -3)   # M 2688
+    assert pick_variant(table, (0, 1, 9, 12, 1280, 9, 12, 1280, 3, 1, False, 11520)) == (3, 2)     # M 108
+    assert pick_variant(table, (0, 4, 72, 96, 320, 72, 96, 320, 3, 1, False, 2880)) == (6, 1)      # M 27648
+    assert pick_variant(table, (0, 1, 1, 2688, 320, 1, 2688, 320, 1, 1, False, 320)) == (18, 4)    # only 1x1 entry
+    assert pick_variant(table, (0, 1, 28, 96, 640, 28, 96, 320, 3, 1, True, 5760)) == (10, 1)      # two-source filter
+    assert pick_variant(table, (1, 1, 28, 96, 320, 56, 192, 320, 3, 1, False, 2880)) == (0, 0)     # no mode-1 entry
+    tie = [((0, 1, 1, 100, 64, 1, 100, 64, 1, 1, False, 64), (1, 1)), ((0, 1, 1, 400, 64, 1, 400, 64, 1, 1, False, 64),
+                                                                      (2, 1))]
+    assert pick_variant(tie, (0, 1, 1, 200, 64, 1, 200, 64, 1, 1, False, 64)) == (1, 1)            # tie: first
+    assert pick_variant([], base) == (0, 0)
