@@ -56,7 +56,30 @@ struct ConvGemmParams {
   long nrows;
   int nmajor;           // tile order within an XCD's range: 0 M-major (row tiles share A), 1 N-major (column
                         // tiles share W; opt-in, DC_GEMM_ORDER=2)
+  // multiply-shift division by hout * wout, wout and hout (fast_div): the pixel -> (frame, y, x) split of
+  // every gathered A row in the prologue is 2 VALU per division instead of a 64-bit division sequence
+  unsigned hw_mul, w_mul, h_mul;
+  int hw_shr, w_shr, h_shr;
 };
+
+// x / d for x < 2^31 by a host-computed (mul, shr) pair (make_fast_div); mul == 0 encodes d == 1
+__device__ __forceinline__ unsigned fast_div(unsigned x, unsigned mul, int shr) {
+  return mul ? (__umulhi(x, mul) >> shr) : x;
+}
+// (mul, shr) with x / d == umulhi(x, mul) >> shr for every x < 2^31, 1 <= d < 2^31 (round-up reciprocal
+// with p = 31 + ceil(log2 d): the error term stays below 2^-31 of the quotient step)
+static void make_fast_div(unsigned d, unsigned& mul, int& shr) {
+  if (d <= 1) {
+    mul = 0;
+    shr = 0;
+    return;
+  }
+  int l = 0;
+  while ((1u << l) < d) ++l;
+  const int pw = 31 + l;
+  mul = (unsigned)(((1ull << pw) + d - 1) / d);
+  shr = pw - 32;
+}
 
 // tile index -> (row tile, column tile) in the launch's rasterisation order
 __device__ __forceinline__ void tile_coords(const ConvGemmParams& p, int tile, int tiles_m, int tiles_n, int& tm,
@@ -213,7 +236,7 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
   const int wm = wid >> 1, wn = wid & 1;
   // wave index as a scalar: the LDS-DMA destination (M0) of every piece is then SALU arithmetic
   const int wid_s = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const long hwo = (long)p.hout * p.wout;
+  const unsigned hwo = (unsigned)(p.hout * p.wout);
   const long M = conv_rows(p);
   const int nkc = max(0, kc_end - kc_begin);
 
@@ -234,20 +257,22 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
     const long m = m0 + row;
     vmask[j] = 0u;
     if constexpr (!SMALLC) {
-      const long mp = m < M ? conv_pix(p, m) : 0;
-      const int n = m < M ? (int)(mp / hwo) : -1;
-      const int rem = m < M ? (int)(mp - (long)n * hwo) : 0;
-      pn[j] = n;
-      poy[j] = rem / p.wout;
-      pox[j] = rem - poy[j] * p.wout;
+      const bool in = m < M;
+      const unsigned mp = in ? (unsigned)conv_pix(p, m) : 0u;
+      const unsigned n = fast_div(mp, p.hw_mul, p.hw_shr);
+      const unsigned rem = mp - n * hwo;
+      const unsigned oy = fast_div(rem, p.w_mul, p.w_shr);
+      pn[j] = in ? (int)n : -1;
+      poy[j] = (int)oy;
+      pox[j] = (int)(rem - oy * (unsigned)p.wout);
       continue;
     }
     int yp[3] = {0, 0, 0}, xp[3] = {0, 0, 0};
     if (m < M) {
-      const long mp = conv_pix(p, m);
-      const int n = (int)(mp / hwo);
-      const int rem = (int)(mp - (long)n * hwo);
-      const int oy = rem / p.wout, ox = rem - (rem / p.wout) * p.wout;
+      const unsigned mp = (unsigned)conv_pix(p, m);
+      const int n = (int)fast_div(mp, p.hw_mul, p.hw_shr);
+      const int rem = (int)(mp - (unsigned)n * hwo);
+      const int oy = (int)fast_div((unsigned)rem, p.w_mul, p.w_shr), ox = rem - oy * p.wout;
       unsigned yv = 0u, xv = 0u;
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
@@ -262,8 +287,8 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
           const int vy = oy - p.pad + t, vx = ox - p.pad + t;
           oky = vy >= 0 && vy < p.hout;
           okx = vx >= 0 && vx < p.wout;
-          iy = oky ? (int)(((long)vy * p.hin) / p.hout) : 0;
-          ix = okx ? (int)(((long)vx * p.win) / p.wout) : 0;
+          iy = oky ? (int)fast_div((unsigned)(vy * p.hin), p.h_mul, p.h_shr) : 0;
+          ix = okx ? (int)fast_div((unsigned)(vx * p.win), p.w_mul, p.w_shr) : 0;
         } else {
           const int ty = oy - 1 + t, tx = ox - 1 + t;
           oky = ty >= 0 && !(ty & 1) && (ty >> 1) < p.hin;
@@ -320,8 +345,8 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
       } else if (p.mode == 1) {
         const int vy = poy[j] - p.pad + ty, vx = pox[j] - p.pad + tx;
         ok = vy >= 0 && vy < p.hout && vx >= 0 && vx < p.wout;
-        iy = ok ? (int)(((long)vy * p.hin) / p.hout) : 0;
-        ix = ok ? (int)(((long)vx * p.win) / p.wout) : 0;
+        iy = ok ? (int)fast_div((unsigned)(vy * p.hin), p.h_mul, p.h_shr) : 0;
+        ix = ok ? (int)fast_div((unsigned)(vx * p.win), p.w_mul, p.w_shr) : 0;
       } else {
         const int yy = poy[j] - 1 + ty, xx = pox[j] - 1 + tx;
         ok = yy >= 0 && !(yy & 1) && (yy >> 1) < p.hin && xx >= 0 && !(xx & 1) && (xx >> 1) < p.win;
@@ -788,6 +813,14 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.mask && p.ldmask % 8 != 0) return DC_ERR_ALIGN;
   if (((uintptr_t)p.x | (uintptr_t)p.x2 | (uintptr_t)p.w | (uintptr_t)p.y) & 15) return DC_ERR_ALIGN;
   if (((uintptr_t)p.resid | (uintptr_t)p.mask) & 15) return DC_ERR_ALIGN;
+  // 32-bit pixel arithmetic in the gather (fast_div): pixel indices and upsample products below 2^31
+  if (p.hin <= 0 || p.win <= 0 || (long)p.nb * p.hout * p.wout >= (1L << 31) ||
+      (long)p.nb * p.hin * p.win >= (1L << 31) || (long)p.hout * p.hin >= (1L << 31) ||
+      (long)p.wout * p.win >= (1L << 31))
+    return DC_ERR_ARG;
+  make_fast_div((unsigned)(p.hout * p.wout), p.hw_mul, p.hw_shr);
+  make_fast_div((unsigned)p.wout, p.w_mul, p.w_shr);
+  make_fast_div((unsigned)p.hout, p.h_mul, p.h_shr);
   const long M = p.rows ? p.nrows : (long)p.nb * p.hout * p.wout;
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
