@@ -813,11 +813,12 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.mask && p.ldmask % 8 != 0) return DC_ERR_ALIGN;
   if (((uintptr_t)p.x | (uintptr_t)p.x2 | (uintptr_t)p.w | (uintptr_t)p.y) & 15) return DC_ERR_ALIGN;
   if (((uintptr_t)p.resid | (uintptr_t)p.mask) & 15) return DC_ERR_ALIGN;
-  // 32-bit pixel arithmetic in the gather (fast_div): pixel indices and upsample products below 2^31
+  // 32-bit pixel arithmetic in the gather (fast_div): pixel indices, and the nearest-upsample source products
+  // (output row / column index x input size, mode 1), below 2^31
   if (p.hin <= 0 || p.win <= 0 || (long)p.nb * p.hout * p.wout >= (1L << 31) ||
-      (long)p.nb * p.hin * p.win >= (1L << 31) || (long)p.hout * p.hin >= (1L << 31) ||
-      (long)p.wout * p.win >= (1L << 31))
+      (long)p.nb * p.hin * p.win >= (1L << 31))
     return DC_ERR_ARG;
+  if (p.mode == 1 && ((long)p.hout * p.hin >= (1L << 31) || (long)p.wout * p.win >= (1L << 31))) return DC_ERR_ARG;
   make_fast_div((unsigned)(p.hout * p.wout), p.hw_mul, p.hw_shr);
   make_fast_div((unsigned)p.wout, p.w_mul, p.w_shr);
   make_fast_div((unsigned)p.hout, p.h_mul, p.h_shr);

@@ -1,11 +1,12 @@
 // GroupNorm(+SiLU) and LayerNorm forward / backward on NHWC rows (gfx950).
 //
 // GroupNorm (diffusers ResnetBlock2D norm1/norm2 + SiLU, Transformer2DModel.norm, conv_norm_out),
-// three launches, all reductions in a fixed order (bitwise reproducible run to run):
-//   stats     per (frame, pixel-chunk) block: 8 channels per thread in registers over its rows,
-//             rows folded through LDS, channels folded into group partials -> slab [nb][nchunk][G][2]
-//   finalize  one block per frame, one wave per group: fold the chunk partials (fp64) -> mean, rstd
-//   apply     elementwise normalise (+ SiLU), 16 B per lane
+// two launches, all reductions in a fixed order (bitwise reproducible run to run):
+//   stats     per (frame, pixel-chunk) block (<= 128 chunks per frame): 8 channels per thread in registers
+//             over its rows, rows folded through LDS, channels folded into group partials -> [nb][nchunk][G][2]
+//   apply     every block first folds its frame's chunk partials (fp64, fixed order) -> mean, rstd, then
+//             normalises (+ SiLU), 16 B per lane.  (DC_GN_FUSED=0: a separate finalize launch, one block per
+//             frame, does the fold instead.)
 // Backward: the same with (sum gamma*dy', sum gamma*dy'*xhat) and dx = rstd*(g*dy' - a - xhat*b).
 // Small group slices (UNet levels 2-3) take a single launch instead: one block per (frame, group),
 // see gn_group_fwd_kernel.
@@ -25,7 +26,8 @@ struct GNShape {
   int nb, hw, c, groups, cpg;
   int rows_per_chunk, nchunk;
   int apply_rows;  // rows per block of the elementwise passes
-  int cgs, R;  // colgroups (c/8) and parallel rows per block
+  int cgs, R;  // colgroups (c/8) and parallel rows per block of the elementwise passes
+  int Rs;      // parallel rows per block of the statistics passes (cgs * Rs <= 1024 threads)
 };
 
 __device__ __forceinline__ void gn_load8(const GNShape& s, int n, int row, int c, float* f) {
@@ -34,13 +36,27 @@ __device__ __forceinline__ void gn_load8(const GNShape& s, int n, int row, int c
   load8(src, f);
 }
 
+// group of each of a thread's 8 channels c0 .. c0 + 7: one division per thread instead of eight (the
+// elementwise passes are short enough that the per-thread setup shows in their time)
+__device__ __forceinline__ void gn_groups8(int c0, int cpg, int (&g)[8]) {
+  int q = c0 / cpg, r = c0 - q * cpg;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    g[k] = q;
+    if (++r == cpg) {
+      r = 0;
+      ++q;
+    }
+  }
+}
+
 // fold per-thread channel partials (a, b)[8] across the R row-lanes, then into group partials
 __device__ void gn_block_fold(const GNShape& s, const float* a, const float* b, float* sh, float* out) {
-  // sh: [2][R][c] floats
+  // sh: [2][Rs][c] floats
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
-  const bool active = r0 < s.R;
+  const bool active = r0 < s.Rs;
   float* sa = sh;
-  float* sb = sh + s.R * s.c;
+  float* sb = sh + s.Rs * s.c;
   if (active) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -52,7 +68,7 @@ __device__ void gn_block_fold(const GNShape& s, const float* a, const float* b, 
   // per channel: sum over row-lanes (fixed order) -> reuse row 0
   for (int ch = threadIdx.x; ch < s.c; ch += blockDim.x) {
     float ta = 0.0f, tb = 0.0f;
-    for (int r = 0; r < s.R; ++r) { ta += sa[r * s.c + ch]; tb += sb[r * s.c + ch]; }
+    for (int r = 0; r < s.Rs; ++r) { ta += sa[r * s.c + ch]; tb += sb[r * s.c + ch]; }
     sa[ch] = ta;
     sb[ch] = tb;
   }
@@ -65,18 +81,82 @@ __device__ void gn_block_fold(const GNShape& s, const float* a, const float* b, 
   }
 }
 
+// (sum, sumsq) -> (mean, rstd) [mode 0] or (sum a / cnt, sum b / cnt) [mode 1] of one group
+__device__ __forceinline__ void gn_final_pair(double ta, double tb, double cnt, float eps, int mode, float* dst) {
+  if (mode == 0) {
+    const double mu = ta / cnt;
+    double var = tb / cnt - mu * mu;
+    if (var < 0.0) var = 0.0;
+    dst[0] = (float)mu;
+    dst[1] = (float)(1.0 / sqrt(var + (double)eps));
+  } else {
+    dst[0] = (float)(ta / cnt);
+    dst[1] = (float)(tb / cnt);
+  }
+}
+
+// Finalize at the head of the elementwise pass (no finalize launch): every block folds its frame's nchunk
+// [G][2] chunk partials into grp[G][2] (LDS).  Thread t owns group pair t % GP (GP = G / 2, one 16-B
+// vector per chunk) and sums chunks t / GP, t / GP + nthr / GP, ... in fp64 (8 vectors in flight); the
+// nthr / GP column sums are then added in thread order.  The order is fixed, so every block -- and every
+// run -- gets the same bits.  Needs G even and blockDim % GP == 0 (gn_fold_ok).  red: blockDim x 4 doubles.
+__device__ void gn_fold_in_block(const GNShape& s, const float* part_n, int mode, float eps, double* red,
+                                 float* grp) {
+  const int GP = s.groups >> 1, nthr = blockDim.x, tid = threadIdx.x;
+  const int gp = tid % GP, cstep = nthr / GP;
+  double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+  for (int c0 = tid / GP; c0 < s.nchunk; c0 += 8 * cstep) {
+    f32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ch = c0 + j * cstep;
+      v[j] = ch < s.nchunk ? *reinterpret_cast<const f32x4*>(part_n + (long)ch * s.groups * 2 + gp * 4)
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      a0 += v[j][0];
+      b0 += v[j][1];
+      a1 += v[j][2];
+      b1 += v[j][3];
+    }
+  }
+  red[tid * 4 + 0] = a0;
+  red[tid * 4 + 1] = b0;
+  red[tid * 4 + 2] = a1;
+  red[tid * 4 + 3] = b1;
+  __syncthreads();
+  if (tid < s.groups) {
+    const int pr = tid >> 1, h = (tid & 1) * 2;
+    double ta = 0.0, tb = 0.0;
+    for (int j = pr; j < nthr; j += GP) {
+      ta += red[j * 4 + h];
+      tb += red[j * 4 + h + 1];
+    }
+    gn_final_pair(ta, tb, (double)s.hw * s.cpg, eps, mode, grp + tid * 2);
+  }
+  __syncthreads();
+}
+
 __global__ void gn_stats_kernel(GNShape s, float* part) {
   extern __shared__ float sh[];
   const int n = blockIdx.y, chunk = blockIdx.x;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (r0 < s.R) {
+  if (r0 < s.Rs) {
     const int rbeg = chunk * s.rows_per_chunk, rend = min(s.hw, rbeg + s.rows_per_chunk);
-    for (int row = rbeg + r0; row < rend; row += s.R) {
-      float f[8];
+    // two rows' loads in flight per iteration; accumulation in row order
+    for (int row = rbeg + r0; row < rend; row += 2 * s.Rs) {
+      const bool two = row + s.Rs < rend;
+      float f[8], f2[8];
       gn_load8(s, n, row, cg * 8, f);
+      if (two) gn_load8(s, n, row + s.Rs, cg * 8, f2);
 #pragma unroll
       for (int i = 0; i < 8; ++i) { a[i] += f[i]; b[i] += f[i] * f[i]; }
+      if (two) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { a[i] += f2[i]; b[i] += f2[i] * f2[i]; }
+      }
     }
   }
   gn_block_fold(s, a, b, sh, part + ((long)n * s.nchunk + chunk) * s.groups * 2);
@@ -112,36 +192,36 @@ __global__ void gn_finalize_kernel(GNShape s, const float* part, float eps, int 
       ta += __shfl_xor(ta, o, 64);
       tb += __shfl_xor(tb, o, 64);
     }
-    if (lane == 0) {
-      float* dst = out + ((long)n * s.groups + g) * 2;
-      if (mode == 0) {
-        const double mu = ta / cnt;
-        double var = tb / cnt - mu * mu;
-        if (var < 0.0) var = 0.0;
-        dst[0] = (float)mu;
-        dst[1] = (float)(1.0 / sqrt(var + (double)eps));
-      } else {
-        dst[0] = (float)(ta / cnt);
-        dst[1] = (float)(tb / cnt);
-      }
-    }
+    if (lane == 0) gn_final_pair(ta, tb, cnt, eps, mode, out + ((long)n * s.groups + g) * 2);
   }
 }
 
 // Elementwise passes: block (chunk, frame) with the stats kernel's thread layout -- each thread keeps
 // one 8-channel group (cg = tid % cgs) over rows r0, r0 + R, ... -- so the per-channel coefficients
 // are computed once per thread and the row loop carries no divisions.
-__global__ void gn_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
-                                bf16* y, int ldy) {
+// part != nullptr: the block first folds the frame's chunk partials itself (gn_fold_in_block) and block 0 of
+// the frame stores (mean, rstd) to stats for the backward; otherwise stats comes from gn_finalize_kernel.
+__global__ void gn_apply_kernel(GNShape s, const float* part, float eps, float* stats, const float* gamma,
+                                const float* beta, int silu, bf16* y, int ldy) {
+  extern __shared__ double gsh[];
   const int n = blockIdx.y;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
+  const float* st = stats + (long)n * s.groups * 2;
+  if (part) {
+    float* grp = reinterpret_cast<float*>(gsh + blockDim.x * 4);
+    gn_fold_in_block(s, part + (long)n * s.nchunk * s.groups * 2, 0, eps, gsh, grp);
+    if (blockIdx.x == 0 && threadIdx.x < s.groups * 2) stats[(long)n * s.groups * 2 + threadIdx.x] = grp[threadIdx.x];
+    st = grp;
+  }
   if (r0 >= s.R) return;
   float mu[8], rs[8], ga[8], be[8];
+  int gk[8];
+  gn_groups8(cg * 8, s.cpg, gk);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = cg * 8 + k, g = c / s.cpg;
-    mu[k] = stats[((long)n * s.groups + g) * 2];
-    rs[k] = stats[((long)n * s.groups + g) * 2 + 1];
+    const int c = cg * 8 + k, g = gk[k];
+    mu[k] = st[g * 2];
+    rs[k] = st[g * 2 + 1];
     ga[k] = gamma[c];
     be[k] = beta[c];
   }
@@ -167,19 +247,21 @@ __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* 
   const int n = blockIdx.y, chunk = blockIdx.x;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
   float a[8] = {0, 0, 0, 0, 0, 0, 0, 0}, b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (r0 < s.R) {
+  if (r0 < s.Rs) {
     // per-thread channel coefficients, once (the row loop carries no divisions or table loads)
     float mu[8], rsd[8], ga[8], be[8];
+    int gk[8];
+    gn_groups8(cg * 8, s.cpg, gk);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int c = cg * 8 + i, g = c / s.cpg;
+      const int c = cg * 8 + i, g = gk[i];
       mu[i] = stats[((long)n * s.groups + g) * 2];
       rsd[i] = stats[((long)n * s.groups + g) * 2 + 1];
       ga[i] = gamma[c];
       be[i] = beta[c];
     }
     const int rbeg = chunk * s.rows_per_chunk, rend = min(s.hw, rbeg + s.rows_per_chunk);
-    for (int row = rbeg + r0; row < rend; row += s.R) {
+    for (int row = rbeg + r0; row < rend; row += s.Rs) {
       float f[8], d[8];
       gn_load8(s, n, row, cg * 8, f);
       load8(dy + ((long)n * s.hw + row) * lddy + cg * 8, d);
@@ -200,20 +282,31 @@ __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* 
   gn_block_fold(s, a, b, sh, part + ((long)n * s.nchunk + chunk) * s.groups * 2);
 }
 
+// part != nullptr: (ma, mb) folded by the block itself from the frame's chunk partials (gn_fold_in_block),
+// otherwise read from ab (gn_finalize_kernel)
 __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
-                                    const bf16* dy, int lddy, const float* ab, bf16* dx, int lddx,
+                                    const bf16* dy, int lddy, const float* part, const float* ab, bf16* dx, int lddx,
                                     const bf16* add1, int ldadd1, const bf16* add2, int ldadd2) {
+  extern __shared__ double gsh[];
   const int n = blockIdx.y;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
+  const float* abn = ab + (long)n * s.groups * 2;
+  if (part) {
+    float* grp = reinterpret_cast<float*>(gsh + blockDim.x * 4);
+    gn_fold_in_block(s, part + (long)n * s.nchunk * s.groups * 2, 1, 0.0f, gsh, grp);
+    abn = grp;
+  }
   if (r0 >= s.R) return;
   float mu[8], rs[8], ga[8], be[8], ma[8], mb[8];
+  int gk[8];
+  gn_groups8(cg * 8, s.cpg, gk);
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = cg * 8 + k, g = c / s.cpg;
+    const int c = cg * 8 + k, g = gk[k];
     mu[k] = stats[((long)n * s.groups + g) * 2];
     rs[k] = stats[((long)n * s.groups + g) * 2 + 1];
-    ma[k] = ab[((long)n * s.groups + g) * 2];
-    mb[k] = ab[((long)n * s.groups + g) * 2 + 1];
+    ma[k] = abn[g * 2];
+    mb[k] = abn[g * 2 + 1];
     ga[k] = gamma[c];
     be[k] = beta[c];
   }
@@ -482,10 +575,12 @@ bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2,
   s.cpg = c / groups;
   s.cgs = c / 8;
   s.R = max(1, 256 / s.cgs);
-  // ~256-512 blocks over the whole launch, each at least R rows
-  const int target_blocks = max(1, 384 / nb);
-  s.rows_per_chunk = max(s.R, (hw + target_blocks - 1) / target_blocks);
-  s.rows_per_chunk = ((s.rows_per_chunk + s.R - 1) / s.R) * s.R;
+  // statistics: up to 1024-thread blocks (the block fold's LDS, 2 Rs c floats, stays <= 64 KB), at most 128
+  // chunks per frame so that the elementwise pass can fold a frame's partials itself (gn_fold_in_block)
+  s.Rs = max(1, 1024 / s.cgs);
+  const int target_blocks = max(8, min(128, 512 / nb));
+  s.rows_per_chunk = max(s.Rs, (hw + target_blocks - 1) / target_blocks);
+  s.rows_per_chunk = ((s.rows_per_chunk + s.Rs - 1) / s.Rs) * s.Rs;
   s.nchunk = (hw + s.rows_per_chunk - 1) / s.rows_per_chunk;
   // elementwise passes: ~1024 blocks over the launch, at least R and at most 64 rows per block
   const int bpf = max(1, 1024 / nb);
@@ -496,6 +591,17 @@ bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2,
 
 // workspace layout: [partials nb*nchunk*G*2][ab nb*G*2]
 inline long gn_part_floats(const GNShape& s) { return (long)s.nb * s.nchunk * s.groups * 2; }
+
+// The elementwise pass folds the partials itself (two launches) when G is even and its block is a multiple
+// of G / 2 threads; DC_GN_FUSED=0 keeps the separate finalize launch (A/B and tests).  Returns the dynamic
+// LDS of the elementwise pass (0: separate finalize).
+size_t gn_fold_lds(const GNShape& s) {
+  if (const char* env = getenv("DC_GN_FUSED"))
+    if (atoi(env) == 0) return 0;
+  const int threads = s.cgs * s.R;
+  if (s.groups % 2 || threads % (s.groups / 2)) return 0;
+  return (size_t)threads * 4 * sizeof(double) + (size_t)s.groups * 2 * sizeof(float);
+}
 
 // Single-launch path selection: widest vector (8 / 4 / 2 channels) that divides the group and keeps
 // every operand aligned; 0 = take the 3-launch form.  Taken when the group slice of each stashed tensor
@@ -563,12 +669,15 @@ extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2
     DC_CHECK_LAUNCH();
     return DC_OK;
   }
-  const int threads = s.cgs * s.R;
-  const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, ws);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, eps, 0, stats);
+  const int threads = s.cgs * s.R, sthreads = s.cgs * s.Rs;
+  const size_t lds = 2 * (size_t)s.Rs * s.c * sizeof(float);
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(s.nchunk, nb), dim3(sthreads), lds, st, s, ws);
+  const size_t flds = gn_fold_lds(s);
+  if (!flds)
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, eps, 0, stats);
   const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
-  hipLaunchKernelGGL(gn_apply_kernel, agrid, dim3(threads), 0, st, s, stats, gamma, beta, silu, (bf16*)y, ldy);
+  hipLaunchKernelGGL(gn_apply_kernel, agrid, dim3(threads), flds, st, s, flds ? ws : nullptr, eps, stats, gamma,
+                     beta, silu, (bf16*)y, ldy);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -598,16 +707,17 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
     DC_CHECK_LAUNCH();
     return DC_OK;
   }
-  const int threads = s.cgs * s.R;
-  const size_t lds = 2 * (size_t)s.R * s.c * sizeof(float);
+  const int threads = s.cgs * s.R, sthreads = s.cgs * s.Rs;
+  const size_t lds = 2 * (size_t)s.Rs * s.c * sizeof(float);
   float* ab = ws + gn_part_floats(s);
-  hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(threads), lds, st, s, stats, gamma, beta, silu,
+  hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(s.nchunk, nb), dim3(sthreads), lds, st, s, stats, gamma, beta, silu,
                      (const bf16*)dy, lddy, ws);
-  hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
+  const size_t flds = gn_fold_lds(s);
+  if (!flds) hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, 0.0f, 1, ab);
   const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
-  hipLaunchKernelGGL(gn_bwd_apply_kernel, agrid, dim3(threads), 0, st, s, stats, gamma, beta, silu,
-                     (const bf16*)dy, lddy, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1, (const bf16*)add2,
-                     ldadd2);
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, agrid, dim3(threads), flds, st, s, stats, gamma, beta, silu,
+                     (const bf16*)dy, lddy, flds ? ws : nullptr, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1,
+                     (const bf16*)add2, ldadd2);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

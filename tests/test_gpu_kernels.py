@@ -85,6 +85,19 @@ def test_conv_epilogues_and_concat(ctx):
     assert rel(nchw(y, n, h, w), ref) < 1e-2
 
 
+def test_linear_many_rows(ctx):
+    """A linear over more rows than sqrt(2^31) (the batch-8 level-0 token count): the gather's 32-bit pixel
+    arithmetic bounds pixel indices, and only the mode-1 upsample products beyond that."""
+    from depth_completion_amd import ops
+    rows, k, m = 55296, 64, 64
+    a = rnd(rows, k, seed=60).to(torch.bfloat16)
+    wl = rnd(m, k, scale=1 / 8, seed=61).to(torch.bfloat16)
+    out = torch.empty(rows, m, dtype=torch.bfloat16, device=dev)
+    ops.linear(ctx, a, wl, rows, m, out)
+    torch.cuda.synchronize()
+    assert rel(out, a.float() @ wl.float().t()) < 1e-2
+
+
 def test_conv_upsample_mode(ctx):
     from depth_completion_amd import ops
     from depth_completion_amd.weights import pack_conv
@@ -181,12 +194,13 @@ def test_small_cin_and_splitk_linear(ctx):
 
 
 # ----------------------------------------------------------------------------- norms
-@pytest.fixture(params=["group", "3pass"])
+@pytest.fixture(params=["group", "2pass", "3pass"])
 def gn_path(request, monkeypatch):
     """GroupNorm launch form: one block per (frame, group) in a single launch wherever the slice fits
-    the LDS (DC_GN_GROUP=-1; by default only small slices take it), or the stats / finalize / apply
-    launches (DC_GN_GROUP=0)."""
-    monkeypatch.setenv("DC_GN_GROUP", "0" if request.param == "3pass" else "-1")   # -1: no size cap
+    the LDS (DC_GN_GROUP=-1; by default only small slices take it), stats + apply with the finalize folded
+    into every apply block (DC_GN_GROUP=0), or stats / finalize / apply (DC_GN_GROUP=0, DC_GN_FUSED=0)."""
+    monkeypatch.setenv("DC_GN_GROUP", "-1" if request.param == "group" else "0")   # -1: no size cap
+    monkeypatch.setenv("DC_GN_FUSED", "0" if request.param == "3pass" else "1")
     return request.param
 
 
@@ -226,8 +240,8 @@ def test_groupnorm_fwd_bwd(ctx, gn_path, c, silu, two):
 
 @pytest.mark.parametrize("n,h,w,c", [(1, 72, 96, 320), (3, 24, 32, 640), (8, 18, 24, 1280), (1, 1, 5, 64)])
 def test_groupnorm_many_chunks(ctx, gn_path, n, h, w, c):
-    """GroupNorm where the stats pass spans many blocks (the last-arriving block folds every chunk
-    partial): statistics against torch fp32, and repeated calls bit-identical (counter reset)."""
+    """GroupNorm where the stats pass spans many blocks (every apply block folds the frame's chunk
+    partials): statistics against torch fp32, and repeated calls bit-identical."""
     from depth_completion_amd import ops
     x = (rnd(n, c, h, w, seed=40) * 1.5 - 0.3).to(torch.bfloat16).float()
     gamma = (1 + 0.1 * rnd(c, seed=41)).to(torch.bfloat16).float()
@@ -263,8 +277,9 @@ def test_groupnorm_paths_agree(ctx, monkeypatch, n, h, w, c, two):
     xa, xb = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if two else (xs, None)
     gy = nhwc(rnd(n, c, h, w, seed=46).to(torch.bfloat16))
     res = {}
-    for path in ("group", "3pass"):
-        monkeypatch.setenv("DC_GN_GROUP", "0" if path == "3pass" else "-1")
+    for path in ("group", "2pass", "3pass"):
+        monkeypatch.setenv("DC_GN_GROUP", "-1" if path == "group" else "0")
+        monkeypatch.setenv("DC_GN_FUSED", "0" if path == "3pass" else "1")
         y = torch.empty_like(xs)
         stats = torch.empty(n, 32, 2, device=dev)
         dx = torch.empty_like(xs)
@@ -273,10 +288,15 @@ def test_groupnorm_paths_agree(ctx, monkeypatch, n, h, w, c, two):
         ops.groupnorm_bwd(ctx, xa, n, h * w, c, gamma, beta, True, stats, gy, dx, **kw)
         torch.cuda.synchronize()
         res[path] = (y.float(), stats.clone(), dx.float())
-    (y1, s1, d1), (y2, s2, d2) = res["group"], res["3pass"]
+    (y1, s1, d1), (y2, s2, d2), (y3, s3, d3) = res["group"], res["3pass"], res["2pass"]
     assert rel(s1, s2) < 1e-5
     assert rel(y1, y2) < 2e-3
     assert rel(d1, d2) < 5e-3
+    # finalize folded into the apply blocks vs the finalize launch: the same fp32 partials, fp64 folds in two
+    # fixed orders
+    assert rel(s3, s2) < 1e-6
+    assert rel(y3, y2) < 2e-3
+    assert rel(d3, d2) < 5e-3
 
 
 @pytest.mark.parametrize("c", [64, 320, 1280])
