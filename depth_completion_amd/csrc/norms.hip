@@ -25,6 +25,7 @@ struct GNShape {
   int ldx, ldx2, c1;
   int nb, hw, c, groups, cpg;
   int rows_per_chunk, nchunk;
+  int pf;      // elementwise passes: first row's loads issued ahead of the in-block partial fold (DC_GN_PF=0: off)
   int apply_rows;  // rows per block of the elementwise passes
   int cgs, R;  // colgroups (c/8) and parallel rows per block of the elementwise passes
   int Rs;      // parallel rows per block of the statistics passes (cgs * Rs <= 1024 threads)
@@ -207,6 +208,11 @@ __global__ void gn_apply_kernel(GNShape s, const float* part, float eps, float* 
   const int n = blockIdx.y;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
   const float* st = stats + (long)n * s.groups * 2;
+  const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows), row0 = rbeg + r0;
+  // the first row's loads go out with the fold's partial loads: one memory round trip before the first barrier
+  const bool pf = s.pf && part && r0 < s.R && row0 < rend;
+  float f0[8];
+  if (pf) gn_load8(s, n, row0, cg * 8, f0);
   if (part) {
     float* grp = reinterpret_cast<float*>(gsh + blockDim.x * 4);
     gn_fold_in_block(s, part + (long)n * s.nchunk * s.groups * 2, 0, eps, gsh, grp);
@@ -225,10 +231,14 @@ __global__ void gn_apply_kernel(GNShape s, const float* part, float eps, float* 
     ga[k] = gamma[c];
     be[k] = beta[c];
   }
-  const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows);
-  for (int row = rbeg + r0; row < rend; row += s.R) {
+  for (int row = row0; row < rend; row += s.R) {
     float f[8];
-    gn_load8(s, n, row, cg * 8, f);
+    if (pf && row == row0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = f0[k];
+    } else {
+      gn_load8(s, n, row, cg * 8, f);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float v = (f[k] - mu[k]) * rs[k] * ga[k] + be[k];
@@ -291,6 +301,13 @@ __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* 
   const int n = blockIdx.y;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
   const float* abn = ab + (long)n * s.groups * 2;
+  const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows), row0 = rbeg + r0;
+  const bool pf = s.pf && part && r0 < s.R && row0 < rend;  // as gn_apply_kernel
+  float f0[8], d0[8];
+  if (pf) {
+    gn_load8(s, n, row0, cg * 8, f0);
+    load8(dy + ((long)n * s.hw + row0) * lddy + cg * 8, d0);
+  }
   if (part) {
     float* grp = reinterpret_cast<float*>(gsh + blockDim.x * 4);
     gn_fold_in_block(s, part + (long)n * s.nchunk * s.groups * 2, 1, 0.0f, gsh, grp);
@@ -310,12 +327,19 @@ __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* 
     ga[k] = gamma[c];
     be[k] = beta[c];
   }
-  const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows);
-  for (int row = rbeg + r0; row < rend; row += s.R) {
+  for (int row = row0; row < rend; row += s.R) {
     const long pix = (long)n * s.hw + row;
     float f[8], d[8], out[8];
-    gn_load8(s, n, row, cg * 8, f);
-    load8(dy + pix * lddy + cg * 8, d);
+    if (pf && row == row0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        f[k] = f0[k];
+        d[k] = d0[k];
+      }
+    } else {
+      gn_load8(s, n, row, cg * 8, f);
+      load8(dy + pix * lddy + cg * 8, d);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float xhat = (f[k] - mu[k]) * rs[k];
@@ -586,6 +610,10 @@ bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2,
   const int bpf = max(1, 1024 / nb);
   s.apply_rows = min(64, max(s.R, (hw + bpf - 1) / bpf));
   s.apply_rows = ((s.apply_rows + s.R - 1) / s.R) * s.R;
+  {
+    const char* e = getenv("DC_GN_PF");  // host side, read per call (graphs capture the choice)
+    s.pf = (e && atoi(e) == 0) ? 0 : 1;
+  }
   return true;
 }
 
