@@ -210,7 +210,9 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
     t_step = max(times[2] - times[1], 1e-3)
     t_fixed = max(times[1] - t_step, 0.0)
     t_frame = (t_fixed + steps * t_step) * seeds
-    return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+    return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads,
+            "cores_label": f"{threads} threads used of {os.cpu_count()} host CPUs visible", "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"oracle bf16 CPU pipeline, 1 frame {w}x{h}, 1- and 2-step calls "
                       f"({times[1]:.1f}s, {times[2]:.1f}s) extrapolated to {steps} guided steps x {seeds} seed(s) "
                       f"({t_step:.2f} s/step incl. weight-grads)"}
@@ -358,10 +360,21 @@ def run_worker(args) -> None:
         dist.barrier()
     mine = time.perf_counter() - t0
     elapsed = max_over_ranks(mine, device=None if dry else dev)
-    per_rank = [mine]
+    # who ran: every rank's (rank, LOCAL_RANK, device PCI address, elapsed) -- the 8-GPU line then shows 8
+    # distinct ranks on 8 distinct devices
+    if dry:
+        devname = "cpu"
+    else:
+        pr = torch.cuda.get_device_properties(dev)
+        devname = (f"{getattr(pr, 'pci_domain_id', 0):04x}:{getattr(pr, 'pci_bus_id', 0):02x}:"
+                   f"{getattr(pr, 'pci_device_id', 0):02x}")
+    me = {"rank": rank, "local_rank": local, "device": devname, "elapsed_s": mine}
+    ranks = [me]
     if world > 1:
-        per_rank = [None] * world
-        dist.all_gather_object(per_rank, mine)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    per_rank = [r["elapsed_s"] for r in ranks]
+    rccl_world = dist.get_world_size() if (world > 1 and dist.is_initialized()) else 1
     assert torch.isfinite(dense).all(), "non-finite dense output"
 
     frames_total = world * args.steps * B
@@ -384,6 +397,9 @@ def run_worker(args) -> None:
                    "weights": "synthetic seeded (Marigold v1-0 UNet + TAESD shapes)",
                    "hip_graph": not args.no_graph, "distinct_frames_per_call": not args.same_frame},
         "per_rank_fps": [round(args.steps * B / t, 4) for t in per_rank],
+        "rccl_world": rccl_world,
+        "ranks": [{"rank": r["rank"], "local_rank": r["local_rank"], "device": r["device"],
+                   "fps": round(args.steps * B / r["elapsed_s"], 4)} for r in ranks],
         "max_over_ranks_s": round(elapsed, 6),
         "frame_roofline": {"algorithmic_tflop_per_frame": round(frame_tflop, 2),
                            "achieved_tflops_per_gpu": round(fps_gpu * frame_tflop, 2),

@@ -84,10 +84,25 @@ std::string read_file(const std::string& path) {
 }
 
 // ------------------------------------------------------------------ device memory owned by the session
+// Move-only: `x = DevMem()` frees x's blocks (a copy would drop them without freeing).
 struct DevMem {
   std::vector<void*> blocks;
-  ~DevMem() {
+  DevMem() = default;
+  DevMem(const DevMem&) = delete;
+  DevMem& operator=(const DevMem&) = delete;
+  DevMem(DevMem&& o) noexcept : blocks(std::move(o.blocks)) { o.blocks.clear(); }
+  DevMem& operator=(DevMem&& o) noexcept {
+    if (this != &o) {
+      release();
+      blocks = std::move(o.blocks);
+      o.blocks.clear();
+    }
+    return *this;
+  }
+  ~DevMem() { release(); }
+  void release() {
     for (void* p : blocks) (void)hipFree(p);
+    blocks.clear();
   }
   void* alloc(size_t bytes, bool zero = true) {
     void* p = nullptr;
@@ -1540,15 +1555,23 @@ int guarded(dc_session* s, void* user_stream, F&& f) {
   try {
     HIPK(hipSetDevice(s->device));
     if (!s->loaded) throw DcError(kErrArg, "no weights loaded (dc_load_weights)");
-    // order the session stream after the caller's work, and the caller's stream after ours
-    hipEvent_t e;
-    HIPK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPK(hipEventRecord(e, (hipStream_t)user_stream));
-    HIPK(hipStreamWaitEvent(s->stream, e, 0));
+    // order the session stream after the caller's work, and the caller's stream after ours -- also when f()
+    // throws after queueing work that reads the caller's buffers (the guard's destructor joins the streams
+    // and destroys the event on every exit path)
+    struct StreamJoin {
+      hipEvent_t e = nullptr;
+      hipStream_t sess, user;
+      ~StreamJoin() {
+        if (!e) return;
+        (void)hipEventRecord(e, sess);
+        (void)hipStreamWaitEvent(user, e, 0);
+        (void)hipEventDestroy(e);
+      }
+    } join{nullptr, s->stream, (hipStream_t)user_stream};
+    HIPK(hipEventCreateWithFlags(&join.e, hipEventDisableTiming));
+    HIPK(hipEventRecord(join.e, (hipStream_t)user_stream));
+    HIPK(hipStreamWaitEvent(s->stream, join.e, 0));
     f();
-    HIPK(hipEventRecord(e, s->stream));
-    HIPK(hipStreamWaitEvent((hipStream_t)user_stream, e, 0));
-    HIPK(hipEventDestroy(e));
     s->err.clear();
     return kOK;
   } catch (const DcError& e) {
@@ -1657,23 +1680,32 @@ extern "C" int dc_load_weights(dc_session* s, const char* dir, const char* tuned
     const int cross = (int)emb.shape.back();
     const int ntok = (int)(emb.numel() / cross);
     if (cross != cfg.cross) throw DcError(kErrArg, "text embedding width != cross_attention_dim");
-    s->unet = UNetW();
-    s->unet.cfg = cfg;
-    s->taesd = TAESDW();
+    // a failed (re)load leaves the session unloaded (never half-loaded): the new weights go into locals and
+    // are swapped in only once everything has loaded
+    s->loaded = false;
     s->plans.clear();
+    s->unet = UNetW();
+    s->taesd = TAESDW();
     s->wmem = DevMem();
+    DevMem wmem;
+    UNetW unet;
+    unet.cfg = cfg;
+    TAESDW taesd;
     {
       SafeTensors ust(d + "/unet/diffusion_pytorch_model.safetensors");
-      Loader L(ust, s->wmem);
-      load_unet(s->unet, L, emb.data, ntok);
+      Loader L(ust, wmem);
+      load_unet(unet, L, emb.data, ntok);
     }
     {
       std::string tp = d + "/taesd/diffusion_pytorch_model.safetensors";
       if (read_file(tp).empty()) tp = d + "/vae/diffusion_pytorch_model.safetensors";
       SafeTensors tst(tp);
-      Loader L(tst, s->wmem);
-      load_taesd(s->taesd, L);
+      Loader L(tst, wmem);
+      load_taesd(taesd, L);
     }
+    s->wmem = std::move(wmem);
+    s->unet = std::move(unet);
+    s->taesd = std::move(taesd);
     s->ex.tuned.clear();
     s->ex.table_keys.clear();
     s->ex.table_choices.clear();
@@ -1725,7 +1757,8 @@ extern "C" int dc_decode_dense(dc_session* s, const void* latents, const float* 
                                int H, int W, const dc_sample_params* p, float* dense_out, void* stream) {
   return guarded(s, stream, [&]() {
     check_params(p);
-    if (!latents || !affine || !sparses || !dense_out || n <= 0) throw DcError(kErrArg, "bad arguments");
+    if (!latents || !affine || !sparses || !dense_out || n <= 0 || H <= 0 || W <= 0)
+      throw DcError(kErrArg, "bad arguments");
     const Geo g = geometry(n, H, W, p->resolution);
     PlanState& st = plan(s, n, g.h, g.w);
     if (st.tab_hw != (long)H * W) {

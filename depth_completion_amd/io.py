@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import concurrent.futures
 import csv
+import os
 from pathlib import Path
 
 import numpy as np
@@ -138,8 +139,14 @@ def filterout(li: list, flags: list[bool]) -> list:
     return [x for x, f in zip(li, flags) if f]
 
 
+def _atomic_path(path: Path) -> Path:
+    """Temporary sibling of ``path`` (same directory and suffix): writers fill it, then os.replace() moves it into
+    place, so an existing output file is always a complete one (predict.py --resume skips existing outputs)."""
+    return path.with_name(f".{path.stem}.{os.getpid()}.tmp{path.suffix}")
+
+
 def save_tensor(x: torch.Tensor, path: Path, compress: str | None = None) -> None:
-    """utils.py:592-689 (.npy / .npz; .bl2 needs blosc2)."""
+    """utils.py:592-689 (.npy / .npz; .bl2 needs blosc2).  Written atomically (temporary file + rename)."""
     path = Path(path)
     path.parent.mkdir(parents=True, exist_ok=True)
     if torch.is_floating_point(x) and x.dtype not in (torch.float32, torch.float64):
@@ -148,16 +155,24 @@ def save_tensor(x: torch.Tensor, path: Path, compress: str | None = None) -> Non
     want = {None: ".npy", "npy": ".npy", "npz": ".npz", "bl2": ".bl2"}[compress]
     if path.suffix != want:
         raise ValueError(f"Invalid extension: {path.suffix} (must be {want})")
-    if compress == "bl2":
-        try:
-            import blosc2
-        except ImportError as e:
-            raise RuntimeError("compress=bl2 needs the blosc2 package, which is not installed") from e
-        blosc2.save_array(arr, str(path), mode="w")
-    elif compress == "npz":
-        np.savez_compressed(path, arr)
-    else:
-        np.save(path, arr)
+    tmp = _atomic_path(path)
+    try:
+        if compress == "bl2":
+            try:
+                import blosc2
+            except ImportError as e:
+                raise RuntimeError("compress=bl2 needs the blosc2 package, which is not installed") from e
+            blosc2.save_array(arr, str(tmp), mode="w")
+        else:
+            with open(tmp, "wb") as f:
+                if compress == "npz":
+                    np.savez_compressed(f, arr)
+                else:
+                    np.save(f, arr)
+        os.replace(tmp, path)
+    finally:
+        if tmp.exists():
+            tmp.unlink()
 
 
 def load_array(path: Path) -> np.ndarray:
@@ -232,4 +247,10 @@ def save_img_tensor(img: torch.Tensor, path: Path) -> None:
     else:
         raise ValueError(f"Unsupported image type: {img.dtype}")
     arr = img.mul(255).add_(0.5).clamp_(0, 255).permute(1, 2, 0).to(torch.uint8).numpy()
-    Image.fromarray(arr.squeeze(-1) if arr.shape[-1] == 1 else arr).save(path)
+    tmp = _atomic_path(path)
+    try:
+        Image.fromarray(arr.squeeze(-1) if arr.shape[-1] == 1 else arr).save(tmp)
+        os.replace(tmp, path)
+    finally:
+        if tmp.exists():
+            tmp.unlink()

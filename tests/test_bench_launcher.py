@@ -27,6 +27,10 @@ def test_two_rank_spawn_prints_one_line():
     assert line["n_gpus"] == 2 and line["steps"] == 2 and line["warmup"] == 1
     assert line["config"]["frames_per_step"] == 6 and line["config"]["parallelism"].startswith("frame-sharded dp2")
     assert len(line["per_rank_fps"]) == 2
+    # the ranks really were distinct processes with distinct LOCAL_RANKs, joined in one process group
+    assert line["rccl_world"] == 2
+    assert sorted(r["local_rank"] for r in line["ranks"]) == [0, 1]
+    assert sorted(r["rank"] for r in line["ranks"]) == [0, 1]
     # value = all ranks' frames over the max-over-ranks time
     assert abs(line["value"] - 2 * 2 * 3 / line["max_over_ranks_s"]) / line["value"] < 0.01
     assert min(line["per_rank_fps"]) * 2 >= line["value"] * 0.99

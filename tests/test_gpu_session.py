@@ -106,6 +106,52 @@ def test_session_errors(tiny_dir):
     assert torch.isfinite(d).all()
 
 
+def test_session_memory_flat_and_failed_reload(tiny_dir, tmp_path):
+    """A long-running session over mixed input sizes, step counts and weight reloads keeps its device memory
+    flat (every DevMem reassignment frees the blocks it replaces), and a reload that fails partway leaves the
+    session unloaded -- the next call reports "no weights loaded" instead of launching on stale pointers."""
+    s = NativeSession(tiny_dir, dev)
+    shapes = ((96, 128), (192, 256))   # same 12 x 16 latent plan at resolution 128, different H * W tables
+    noise = _noise(2024, 12, 16)
+    inputs = {hw: synth_inputs(1, hw[0], hw[1], 40, seed=6) for hw in shapes}
+
+    def sweep():
+        for hw in shapes:
+            for steps in (2, 3):
+                imgs, sparses = inputs[hw]
+                d, _ = s.complete(imgs, sparses, noise, SampleParams.make(steps=steps, resolution=128))
+                lat = torch.zeros(1, 4, 12, 16, dtype=torch.bfloat16, device=dev)
+                aff = torch.tensor([[1.0, 0.0]], device=dev)
+                s.decode_dense(lat, aff, sparses, SampleParams.make(steps=steps, resolution=128))
+        s._check(s.lib.dc_load_weights(s.h, str(tiny_dir).encode(), b""), "dc_load_weights")
+        torch.cuda.synchronize()
+
+    sweep()
+    free0 = torch.cuda.mem_get_info(dev)[0]
+    for _ in range(3):
+        sweep()
+    free1 = torch.cuda.mem_get_info(dev)[0]
+    print(f"\nsession device memory over 3 sweeps: {(free0 - free1) / 2**20:+.1f} MiB")
+    assert free0 - free1 < 8 << 20, (free0, free1)
+    # a reload that fails partway (no UNet safetensors) leaves the session unloaded
+    bad = tmp_path / "bad"
+    (bad / "unet").mkdir(parents=True)
+    import shutil
+    shutil.copy(tiny_dir / "empty_text_embedding.safetensors", bad / "empty_text_embedding.safetensors")
+    with pytest.raises(Exception):
+        s._check(s.lib.dc_load_weights(s.h, str(bad).encode(), b""), "dc_load_weights")
+    imgs, sparses = inputs[shapes[0]]
+    with pytest.raises(ValueError, match="no weights loaded"):
+        s.complete(imgs, sparses, noise, SampleParams.make(steps=2, resolution=128))
+    # ... and a good reload makes it usable again
+    s._check(s.lib.dc_load_weights(s.h, str(tiny_dir).encode(), b""), "dc_load_weights")
+    d, _ = s.complete(imgs, sparses, noise, SampleParams.make(steps=2, resolution=128))
+    assert torch.isfinite(d).all()
+    with pytest.raises(ValueError):
+        s.decode_dense(torch.zeros(1, 4, 12, 16, dtype=torch.bfloat16, device=dev), torch.zeros(1, 2, device=dev),
+                       torch.zeros(1, 1, 0, 0, device=dev), SampleParams.make(steps=2, resolution=128))
+
+
 def test_session_equals_python_pipeline_c2_full_unet(tmp_path):
     """Full Marigold v1-0 UNet at the C2 shape (latent 72x96, tuned GEMM table, stream-K attention, sparse-aware
     decode), 3 guided steps: bitwise equal."""

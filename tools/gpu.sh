@@ -1,0 +1,79 @@
+#!/bin/bash
+# One parameterised GPU-box pass (replaces the per-experiment tools/gpu_r02*.sh one-shots).
+#
+#   bash tools/gpu.sh <tag> <step> [<step> ...]
+#
+# Outputs go to gpurun_out/<tag>/.  Every GPU step runs under its own time limit and the pass stops at the
+# first failing step (set -e): nothing else touches the GPU after a fault, abort or timeout.
+# Steps:
+#   tests[=<pytest -k expr>]   GPU suite (or the selected tests), -s output kept (printed errors)
+#   smoke                      __graft_entry__.smoke()
+#   c2 | c2cpu                 C2 bench line (c2cpu: with the CPU baseline)
+#   c3 | c4 | c4b8 | c5        C3 batch 8, C4 KITTI 64-beam (batch 1 / 8), C5 10-seed ensemble bench lines
+#   trace                      rocprofv3 --kernel-trace --stats of a short C2 bench
+#   trace3                     the same for C3 (batch 8)
+#   pmc                        FETCH_SIZE and WRITE_SIZE passes over the conv kernel (eager C2, 4 denoise steps)
+#   breakdown[=<batch>]        per-shape conv breakdown of one guided step (tools/conv_breakdown.py)
+#   py=<script args>           any repo python script (e.g. py=tools/gemm_one.py --m 6912)
+set -e
+tag=${1:?tag}
+shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  case "$step" in
+    tests)
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread \
+        > "$out/gputest.log" 2>&1 ;;
+    tests=*)
+      timeout -k 10 1200 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread -k "${step#tests=}" \
+        > "$out/gputest_$n.log" 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 ;;
+    c2)
+      timeout -k 10 400 python -u bench.py --no-cpu-baseline > "$out/bench_c2.json" 2> "$out/bench_c2.err" ;;
+    c2cpu)
+      timeout -k 10 600 python -u bench.py > "$out/bench_c2.json" 2> "$out/bench_c2.err" ;;
+    c3)
+      timeout -k 10 400 python -u bench.py --batch 8 --steps 2 --warmup 1 --no-cpu-baseline \
+        > "$out/bench_c3_b8.json" 2> "$out/bench_c3_b8.err" ;;
+    c4)
+      timeout -k 10 300 python -u bench.py --height 352 --width 1216 --pattern beams --no-cpu-baseline \
+        > "$out/bench_c4.json" 2> "$out/bench_c4.err" ;;
+    c4b8)
+      timeout -k 10 300 python -u bench.py --height 352 --width 1216 --pattern beams --batch 8 --steps 2 --warmup 1 \
+        --no-cpu-baseline > "$out/bench_c4_b8.json" 2> "$out/bench_c4_b8.err" ;;
+    c5)
+      timeout -k 10 400 python -u bench.py --height 900 --width 1600 --points 3000 --seeds 10 --steps 2 --warmup 1 \
+        --no-cpu-baseline > "$out/bench_c5.json" 2> "$out/bench_c5.err" ;;
+    trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$out/trace_bench.json" 2> "$out/trace.err" ;;
+    trace3)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace3" -o run --output-format csv -- \
+        python3 bench.py --batch 8 --steps 1 --warmup 1 --no-cpu-baseline > "$out/trace3_bench.json" 2> "$out/trace3.err" ;;
+    pmc)
+      timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex conv_gemm -d "$out/pmc_fetch" -o run \
+        --output-format csv -- python3 bench.py --no-graph --steps 1 --warmup 0 --no-cpu-baseline --denoise-steps 4 \
+        > "$out/pmc_fetch.json" 2> "$out/pmc_fetch.err"
+      timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex conv_gemm -d "$out/pmc_write" -o run \
+        --output-format csv -- python3 bench.py --no-graph --steps 1 --warmup 0 --no-cpu-baseline --denoise-steps 4 \
+        > "$out/pmc_write.json" 2> "$out/pmc_write.err" ;;
+    breakdown)
+      timeout -k 10 300 python -u tools/conv_breakdown.py > "$out/conv_breakdown.txt" 2> "$out/conv_breakdown.err" ;;
+    breakdown=*)
+      timeout -k 10 300 python -u tools/conv_breakdown.py --batch "${step#breakdown=}" \
+        > "$out/conv_breakdown_b${step#breakdown=}.txt" 2> "$out/conv_breakdown.err" ;;
+    py=*)
+      # shellcheck disable=SC2086
+      timeout -k 10 600 python -u ${step#py=} > "$out/py_$n.txt" 2> "$out/py_$n.err" ;;
+    *)
+      echo "unknown step $step" >&2
+      exit 2 ;;
+  esac
+  echo "[$tag] step $n ($step) done"
+done
+echo "[$tag] all done"
