@@ -223,8 +223,9 @@ class OracleMarigoldDC(MarigoldBase):
                  norm="minmax", percentile=(0.01, 0.99), pred_latents_prev=None, beta=0.9, steps=50,
                  resolution=768, closed_form=None, opt="adam", lr=None, kld=False, kld_weight=0.1,
                  kld_mode="simple", interp_mode="bilinear", loss_funcs=None, seed=2024,
-                 train_latents=True, train_method="per-step", train_steps=10, init_noise=None):
-        """marigold_dc.py:467-985.  ``init_noise`` (build extension) overrides the seeded draw."""
+                 train_latents=True, train_method="per-step", train_steps=10, init_noise=None, step_hook=None):
+        """marigold_dc.py:467-985.  ``init_noise`` (build extension) overrides the seeded draw; ``step_hook``
+        (test infrastructure) observes / replays the guided loop per step (see the loop below)."""
         # --- validation (marigold_dc.py:583-656)
         if (imgs.ndim != 4 or sparses.ndim != 4 or imgs.shape[0] != sparses.shape[0]
                 or imgs.shape[-2:] != sparses.shape[-2:]):
@@ -324,9 +325,19 @@ class OracleMarigoldDC(MarigoldBase):
                 raise ValueError(f"Unknown optimizer: {opt}")
 
         # --- denoising loop (marigold_dc.py:791-909)
+        # step_hook (test infrastructure, not in the reference): step_hook("pre", i, t, state) before and
+        # step_hook("post", i, t, state) after each guided step; state = {"lat", "img_lat", "optim", "aff"} (+ "v",
+        # "grad" -- lat.grad after the rescale -- at "post").  A "pre" hook may overwrite lat.data, the optimiser
+        # state or state["img_lat"] in place: the per-step (teacher-forced) parity test replays another
+        # execution's trajectory one step at a time this way.
+        guided_hook = step_hook if (optim is not None and train_method == "per-step") else None
         with (nullcontext() if per_step else torch.no_grad()):
             self.scheduler.set_timesteps(steps, device=self.device)
-            for t in self.scheduler.timesteps:
+            for i, t in enumerate(self.scheduler.timesteps):
+                if guided_hook is not None:
+                    state = {"lat": lat, "img_lat": img_lat, "optim": optim, "aff": aff_params}
+                    guided_hook("pre", i, t, state)
+                    img_lat = state["img_lat"]
                 if optim is not None and train_method == "per-step":
                     optim.zero_grad()
                 v = self._predict_noise(img_lat, lat, t)
@@ -349,6 +360,9 @@ class OracleMarigoldDC(MarigoldBase):
                     optim.step()
                     with torch.no_grad():
                         lat.data = self.scheduler.step(v, t, lat, generator=gen).prev_sample
+                    if guided_hook is not None:
+                        state.update(v=v.detach(), grad=lat.grad.detach())
+                        guided_hook("post", i, t, state)
                 else:
                     lat = self.scheduler.step(v, t, lat, generator=gen).prev_sample
 

@@ -133,7 +133,8 @@ def test_session_memory_flat_and_failed_reload(tiny_dir, tmp_path):
     free1 = torch.cuda.mem_get_info(dev)[0]
     print(f"\nsession device memory over 3 sweeps: {(free0 - free1) / 2**20:+.1f} MiB")
     assert free0 - free1 < 8 << 20, (free0, free1)
-    # a reload that fails partway (no UNet safetensors) leaves the session unloaded
+    # a reload refused by its config checks (no unet/config.json: the Marigold defaults do not match the tiny
+    # embedding) changes nothing: the session keeps its weights
     bad = tmp_path / "bad"
     (bad / "unet").mkdir(parents=True)
     import shutil
@@ -141,6 +142,12 @@ def test_session_memory_flat_and_failed_reload(tiny_dir, tmp_path):
     with pytest.raises(Exception):
         s._check(s.lib.dc_load_weights(s.h, str(bad).encode(), b""), "dc_load_weights")
     imgs, sparses = inputs[shapes[0]]
+    d, _ = s.complete(imgs, sparses, noise, SampleParams.make(steps=2, resolution=128))
+    assert torch.isfinite(d).all()
+    # a reload that fails partway (config fine, no UNet safetensors) leaves the session unloaded
+    shutil.copy(tiny_dir / "unet" / "config.json", bad / "unet" / "config.json")
+    with pytest.raises(Exception):
+        s._check(s.lib.dc_load_weights(s.h, str(bad).encode(), b""), "dc_load_weights")
     with pytest.raises(ValueError, match="no weights loaded"):
         s.complete(imgs, sparses, noise, SampleParams.make(steps=2, resolution=128))
     # ... and a good reload makes it usable again
