@@ -459,15 +459,15 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
 // the tile's counter (agent-scope atomic) after every wave's vmcnt(0); the block that arrives last reads
 // all partials back with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1), leaves their sum in acc
 // and returns true (the caller then runs the epilogue).  slot_of(i) = slab slot of segment i.
-template <int BM, int BN, typename SlotFn>
-__device__ __forceinline__ bool tile_handoff(const ConvGemmParams& p, char* smem, int tile, int my_slot, int narrive,
-                                             SlotFn slot_of, f32x4 (&acc)[BM / 32][BN / 32]) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int MI = WM / 16, NJ = WN / 16;
-  constexpr int TILE_F = BM * BN;
+// (MI x NJ 16x16 accumulators per wave, 4 waves: any wave layout of the tile)
+template <int MI, int NJ, typename SlotFn>
+__device__ __forceinline__ bool tile_handoff_g(const ConvGemmParams& p, char* smem, int tile, int my_slot, int narrive,
+                                               SlotFn slot_of, f32x4 (&acc)[MI][NJ]) {
+  constexpr int WAVE_F = MI * NJ * 256;
+  constexpr int TILE_F = 4 * WAVE_F;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
-  const long slab = (long)my_slot * TILE_F + wid * (WM * WN) + lane * 4;
+  const long slab = (long)my_slot * TILE_F + wid * WAVE_F + lane * 4;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -499,7 +499,7 @@ __device__ __forceinline__ bool tile_handoff(const ConvGemmParams& p, char* smem
 #pragma unroll
       for (int g = 0; g < GS; ++g) {
         if (sp0 + g < narrive) {
-          const long src = (long)slot_of(sp0 + g) * TILE_F + wid * (WM * WN) + lane * 4;
+          const long src = (long)slot_of(sp0 + g) * TILE_F + wid * WAVE_F + lane * 4;
 #pragma unroll
           for (int j = 0; j < NJ; ++j) part[g][j] = load_sc1_x4(rs, src + (i * NJ + j) * 256);
         }
@@ -515,6 +515,11 @@ __device__ __forceinline__ bool tile_handoff(const ConvGemmParams& p, char* smem
   }
   if (tid == 0) p.counters[tile] = 0;  // ready for the next launch (ordered by the kernel boundary)
   return true;
+}
+template <int BM, int BN, typename SlotFn>
+__device__ __forceinline__ bool tile_handoff(const ConvGemmParams& p, char* smem, int tile, int my_slot, int narrive,
+                                             SlotFn slot_of, f32x4 (&acc)[BM / 32][BN / 32]) {
+  return tile_handoff_g<BM / 32, BN / 32>(p, smem, tile, my_slot, narrive, slot_of, acc);
 }
 
 // epilogue: bias in fp32, round to bf16 into a per-wave LDS tile, then 16-B coalesced rows
@@ -683,6 +688,264 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Halo-tile direct 3x3 conv (stride 1, pad 1; mode 0 direct, mode 1 nearest upsample folded in; cin % 64 == 0).
+//
+// The im2col path above fills every 3x3 A row 9 times (once per tap) from L2; at batch 1 the UNet / TAESD convs
+// are bound by that operand fill (32 FLOP per filled byte on a 64x64 tile).  Here a block owns a TH x TW
+// spatial tile of output pixels (one frame) x BN output channels and walks the input channels in 64-wide
+// chunks: per chunk it fills the (TH+2) x (TW+2) halo of the input ONCE into LDS and runs all 9 taps from it
+// (the A fragment of tap (ky, kx) for output pixel (ty, tx) is halo row (ty+ky)(TW+2) + tx+kx: a per-lane LDS
+// address), while the weights stream through an S-deep ring one (tap, chunk) slice of BN x 64 at a time.
+// Per 64-channel chunk that is (TH+2)(TW+2) + 9 BN rows of 128 B for 2 TH TW BN 576 FLOP: 162 FLOP/B at
+// 8x32 x 64 against 32 (64x64 im2col) and 64 (128x128 im2col).
+//
+// Pipeline: iteration i = (chunk c, tap t), i = 9 (c - c_begin) + t.  The halo of chunk c is issued with the
+// weight slice of its tap 0, S - 1 iterations ahead like every weight slice (two halo slots: chunk c + 1's
+// halo lands in the slot chunk c - 1 used, issued no earlier than (c, 1)).  Before iteration i the waves wait
+// (counted vmcnt) until only the loads of iterations i+1 .. i+S-2 may be in flight: that retires iteration
+// i's weights and its chunk's halo; one barrier per iteration.  Input channels split over blocks (split-K)
+// are summed in split order by the last-arriving block (tile_handoff_g).  4 waves, WGM x WGN wave layout;
+// BMP = TH TW padded to whole 16-row fragments per wave (pad rows compute garbage that is never stored).
+template <int TH, int TW, int BN, int WGM, int WGN, int S>
+struct HaloCfg {
+  static_assert(WGM * WGN == 4, "4 waves");
+  static constexpr int BM = TH * TW;
+  static constexpr int BMP = ((BM + 16 * WGM - 1) / (16 * WGM)) * (16 * WGM);
+  static constexpr int WM = BMP / WGM, WN = BN / WGN;
+  static constexpr int MI = WM / 16, NJ = WN / 16;
+  static_assert(WN % 16 == 0 && BN % 32 == 0, "BN");
+  static constexpr int HW2 = TW + 2;
+  static constexpr int HROWS = (TH + 2) * (TW + 2);
+  static constexpr int LH = (HROWS + 31) / 32;   // block-wide 16-B LDS-DMA instructions per thread per halo
+  static constexpr int LW = BN / 32;             // ... per weight slice
+  static constexpr int RB = 128;                 // 64 bf16 channels per LDS row
+  static constexpr int HALO = LH * 32 * RB;
+  static constexpr int WST = BN * RB;
+  static constexpr int RING = 2 * HALO + S * WST;
+  static constexpr int EPI = 4 * WM * (WN + 8) * 2;
+  static constexpr int LDS = RING > EPI ? RING : EPI;
+  static_assert(S >= 2 && S <= 8, "ring depth");
+  static_assert((S - 2) * LW + LH <= 63, "vmcnt range");
+};
+
+// wait until at most k weight slices (+ e halos) issued after the current iteration's loads are in flight
+template <int LW, int LH, int S>
+__device__ __forceinline__ void halo_wait(int k, int e) {
+#define DC_HW(K)                                           \
+  if (k == K) {                                            \
+    if (e) vm_wait<(K) * LW + ((K) > 0 ? LH : 0)>();       \
+    else vm_wait<(K) * LW>();                              \
+    return;                                                \
+  }
+  if constexpr (S >= 8) { DC_HW(6) }
+  if constexpr (S >= 7) { DC_HW(5) }
+  if constexpr (S >= 6) { DC_HW(4) }
+  if constexpr (S >= 5) { DC_HW(3) }
+  if constexpr (S >= 4) { DC_HW(2) }
+  if constexpr (S >= 3) { DC_HW(1) }
+  vm_wait<0>();
+#undef DC_HW
+}
+
+template <int TH, int TW, int BN, int WGM, int WGN, int S>
+__global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) {
+  using C = HaloCfg<TH, TW, BN, WGM, WGN, S>;
+  constexpr int MI = C::MI, NJ = C::NJ, WM = C::WM, WN = C::WN, RB = C::RB, LH = C::LH, LW = C::LW;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  const int wm = wid / WGN, wn = wid % WGN;
+
+  // ---- block -> (split, column tile, frame, tile row, tile column): split-major over the whole grid
+  const int tiles_n = (p.cout + BN - 1) / BN;
+  const int tiles_x = (p.wout + TW - 1) / TW, tiles_y = (p.hout + TH - 1) / TH;
+  const int tiles = gridDim.x, nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+  const int wk = xcd_remap(bid, nblk);
+  const int split = wk / tiles;
+  const int lb = wk - split * tiles;
+  const int sp_tile = lb / tiles_n, tn = lb - (lb / tiles_n) * tiles_n;
+  const int frame = sp_tile / (tiles_y * tiles_x);
+  const int trem = sp_tile - frame * (tiles_y * tiles_x);
+  const int oy0 = (trem / tiles_x) * TH, ox0 = (trem - (trem / tiles_x) * tiles_x) * TW;
+  const int n0 = tn * BN;
+  const int nck = p.cin / 64;
+  const int c_begin = split * p.kps;
+  const int c_end = min(nck, c_begin + p.kps);
+  const int NI = max(0, c_end - c_begin) * 9;
+
+  // ---- per-lane LDS-DMA offsets: halo rows (fixed for the block; the chunk's channel offset rides in soffset)
+  constexpr int kOOB = (int)0x80000000u;
+  const int slot = tid & 7, r0 = tid >> 3;
+  const bool two_src = p.c1 < p.cin;
+  int h_off[LH], h_off2[LH];
+#pragma unroll
+  for (int j = 0; j < LH; ++j) {
+    const int hr = r0 + 32 * j;
+    const int hy = hr / C::HW2, hx = hr - (hr / C::HW2) * C::HW2;
+    const int vy = oy0 - 1 + hy, vx = ox0 - 1 + hx;
+    bool ok = hr < C::HROWS && vy >= 0 && vy < p.hout && vx >= 0 && vx < p.wout;
+    int iy = vy, ix = vx;
+    if (p.mode == 1) {
+      iy = ok ? (int)fast_div((unsigned)(vy * p.hin), p.h_mul, p.h_shr) : 0;
+      ix = ok ? (int)fast_div((unsigned)(vx * p.win), p.w_mul, p.w_shr) : 0;
+    }
+    const int pix = (frame * p.hin + iy) * p.win + ix;
+    const int sw = (slot ^ (hr & 7)) * 8;
+    h_off[j] = ok ? (pix * p.ldx + sw) * 2 : kOOB;
+    h_off2[j] = ok ? (pix * p.ldx2 + sw) * 2 : kOOB;
+  }
+  int b_off[LW];
+#pragma unroll
+  for (int j = 0; j < LW; ++j) {
+    const int row = r0 + 32 * j;
+    const int co = n0 + row;
+    b_off[j] = co < p.cout ? (co * p.ktot + (slot ^ (row & 7)) * 8) * 2 : kOOB;
+  }
+  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(p.x);
+  const __amdgpu_buffer_rsrc_t ra2 = buf_rsrc(p.x2);
+  const __amdgpu_buffer_rsrc_t rb = buf_rsrc(p.w);
+
+  // per-lane halo row of each A fragment at tap (0, 0)
+  int hbase[MI];
+#pragma unroll
+  for (int ii = 0; ii < MI; ++ii) {
+    int pl = wm * WM + ii * 16 + (lane & 15);
+    pl = pl < C::BM ? pl : 0;   // pad rows read a valid halo row; never stored
+    const int ty = pl / TW, tx = pl - (pl / TW) * TW;
+    hbase[ii] = ty * C::HW2 + tx;
+  }
+
+  // issue cursor (scalar): next iteration's chunk / tap
+  int q_i = 0;
+  int q_c = c_begin, q_t = 0;
+  auto issue = [&]() __attribute__((always_inline)) {
+    if (q_t == 0) {
+      DC_LDS char* hb = (DC_LDS char*)smem + ((q_c - c_begin) & 1) * C::HALO;
+      const int ch = q_c * 64;
+      if (ch >= p.c1) {
+#pragma unroll
+        for (int j = 0; j < LH; ++j) buf_load_lds16(ra2, hb + (wid_s * 64 + 256 * j) * 16, h_off2[j], (ch - p.c1) * 2);
+      } else {
+#pragma unroll
+        for (int j = 0; j < LH; ++j) buf_load_lds16(ra, hb + (wid_s * 64 + 256 * j) * 16, h_off[j], ch * 2);
+      }
+    }
+    DC_LDS char* wb = (DC_LDS char*)smem + 2 * C::HALO + (q_i % S) * C::WST;
+    const int koff = (q_t * p.cin + q_c * 64) * 2;
+#pragma unroll
+    for (int j = 0; j < LW; ++j) buf_load_lds16(rb, wb + (wid_s * 64 + 256 * j) * 16, b_off[j], koff);
+    ++q_i;
+    if (++q_t == 9) {
+      q_t = 0;
+      ++q_c;
+    }
+  };
+  (void)two_src;
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int s = 0; s < S - 1 && s < NI; ++s) issue();
+  int tap = 0, cpar = 0;
+  for (int i = 0; i < NI; ++i) {
+    // loads younger than iteration i's: iterations i+1 .. min(i+S-2, NI-1); one of them may carry a halo
+    const int last = min(i + S - 2, NI - 1);
+    const int k = last - i;
+    const int e = (k > 0 && (tap + k) >= 9) ? 1 : 0;
+    halo_wait<LW, LH, S>(k, e);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (i + S - 1 < NI) issue();
+    const char* ha = smem + cpar * C::HALO;
+    const char* wbase = smem + 2 * C::HALO + (i % S) * C::WST;
+    const int ky = tap >= 6 ? 2 : (tap >= 3 ? 1 : 0);
+    const int toff = ky * C::HW2 + (tap - 3 * ky);
+    bf16x8 af[2][MI], bfr[2][NJ];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = ks * 4 + (lane >> 4);
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii) {
+        const int r = hbase[ii] + toff;
+        af[ks][ii] = *reinterpret_cast<const bf16x8*>(ha + r * RB + ((chunk ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        const int row = wn * WN + jj * 16 + (lane & 15);
+        bfr[ks][jj] = *reinterpret_cast<const bf16x8*>(wbase + row * RB + ((chunk ^ (row & 7)) << 4));
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj)
+          acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][ii], bfr[ks][jj], acc[ii][jj], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
+    if (++tap == 9) {
+      tap = 0;
+      cpar ^= 1;
+    }
+  }
+  vm_wait<0>();
+
+  if (p.splits > 1 &&
+      !tile_handoff_g<MI, NJ>(p, smem, lb, split * tiles + lb, p.splits, [&](int sp) { return sp * tiles + lb; }, acc))
+    return;
+
+  // ---- epilogue: bias in fp32, bf16 per-wave LDS tile, then 16-B rows mapped to the tile's output pixels
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  __syncthreads();
+  constexpr int LDE = WN + 8;
+  bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = n0 + wn * WN + j * 16 + col_l;
+    const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) es[(i * 16 + row_l + q) * LDE + j * 16 + col_l] = (bf16)(acc[i][j][q] + bv);
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  constexpr int GPR = WN / 8;
+#pragma unroll 4
+  for (int g = lane; g < WM * GPR; g += 64) {
+    const int row = g / GPR, cg = g - (g / GPR) * GPR;
+    const int pl = wm * WM + row;
+    const int c = n0 + wn * WN + cg * 8;
+    const int ty = pl / TW, tx = pl - (pl / TW) * TW;
+    const int oy = oy0 + ty, ox = ox0 + tx;
+    if (pl >= C::BM || oy >= p.hout || ox >= p.wout || c >= p.cout) continue;
+    float v[8];
+    load8(es + row * LDE + cg * 8, v);
+    epilogue_store(p, ((long)frame * p.hout + oy) * p.wout + ox, c, v, false);
+  }
+}
+
+// halo variants: (TH, TW, BN, wave layout WGM x WGN, weight ring depth S)
+struct HaloAlgo {
+  int th, tw, bn, wgm, wgn, s;
+};
+constexpr HaloAlgo kHaloAlgos[] = {
+    {8, 32, 64, 4, 1, 4},   // 256 px x 64: TAESD 64-channel levels, UNet level 0
+    {4, 32, 64, 2, 2, 3},   // 128 px x 64 at 2 blocks / CU
+    {4, 32, 32, 4, 1, 4},   // 128 px x 32
+    {8, 16, 64, 4, 1, 4},   // 128 px x 64, 16 wide (level 1: 48 columns)
+    {6, 24, 64, 1, 4, 4},   // 144 px x 64 (level 2: 18 x 24)
+    {9, 12, 64, 1, 4, 4},   // 108 px x 64 (level 3: 9 x 12, the whole frame)
+    {9, 12, 32, 2, 2, 4},   // 108 px x 32 (level 3)
+    {8, 24, 32, 2, 2, 4},   // 192 px x 32 (level 2)
+};
+
 constexpr long kCounterBytes = 64 * 1024;
 constexpr int kMaxSplitTiles = (int)(kCounterBytes / 4);
 
@@ -699,6 +962,43 @@ constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 
                            // block per CU is bound by the bytes it keeps in flight
                            {64, 64, 64, 8},    {128, 64, 64, 6},  {64, 128, 64, 6}, {64, 64, 32, 8}};
 constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
+constexpr int kNumHalo = sizeof(kHaloAlgos) / sizeof(kHaloAlgos[0]);
+constexpr int kNumAll = kNumAlgos + kNumHalo;   // algo ids kNumAlgos + 1 .. kNumAll: halo variants
+static_assert(kNumHalo == 8, "DC_HALO cases below");
+
+template <int TH, int TW, int BN, int WGM, int WGN, int S>
+int launch_halo(ConvGemmParams& p, int splits, hipStream_t stream) {
+  using Cf = HaloCfg<TH, TW, BN, WGM, WGN, S>;
+  const long tiles_l = (long)p.nb * ((p.hout + TH - 1) / TH) * ((p.wout + TW - 1) / TW) * ((p.cout + BN - 1) / BN);
+  if (tiles_l >= (1L << 30)) return DC_ERR_ARG;
+  const int tiles = (int)tiles_l;
+  const int nck = p.cin / 64;
+  p.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(p.ws) + (p.ws_bytes - kCounterBytes));
+  splits = max(1, min(splits, nck));   // stream-K requests (< 0) run unsplit
+  if (p.ws == nullptr || tiles > kMaxSplitTiles) splits = 1;
+  while (splits > 1 && (long)splits * tiles * Cf::BMP * BN * 4 > p.ws_bytes - kCounterBytes) --splits;
+  p.kps = (nck + splits - 1) / splits;
+  splits = (nck + p.kps - 1) / p.kps;
+  p.splits = splits;
+  p.sk_blocks = 0;
+  hipLaunchKernelGGL((conv_halo_kernel<TH, TW, BN, WGM, WGN, S>), dim3(tiles, splits), dim3(256), 0, stream, p);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+// the halo kernel's contract: 3x3, stride 1, pad 1, direct (input = output size) or nearest-upsample input,
+// whole 64-channel chunks (both concat sources), no row list / GEGLU epilogue, 32-bit byte offsets
+bool halo_eligible(const ConvGemmParams& p) {
+  if (p.kh != 3 || p.kw != 3 || p.stride != 1 || p.pad != 1 || p.rows || p.geglu) return false;
+  if (p.cin % 64 != 0 || p.ktot != 9 * p.cin) return false;
+  if (p.c1 < p.cin && p.c1 % 64 != 0) return false;
+  if (p.mode == 0 && (p.hin != p.hout || p.win != p.wout)) return false;
+  if (p.mode != 0 && p.mode != 1) return false;
+  const long ld = p.ldx > p.ldx2 ? p.ldx : p.ldx2;
+  if ((long)p.nb * p.hin * p.win * ld * 2 >= (1L << 31)) return false;
+  if ((long)p.cout * p.ktot * 2 >= (1L << 31)) return false;
+  return true;
+}
 
 template <int BM, int BN, int BK, int S>
 int launch_algo(ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t stream) {
@@ -758,7 +1058,7 @@ void auto_algo(long M, int cout, int nk, int& algo, int& splits) {
 
 }  // namespace
 
-extern "C" int dc_conv_num_algos(void) { return kNumAlgos; }
+extern "C" int dc_conv_num_algos(void) { return kNumAll; }
 
 extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (!d || !d->x || !d->w || !d->y) return DC_ERR_ARG;
@@ -805,7 +1105,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
-  if (d->algo < 0 || d->algo > kNumAlgos || d->splitk < -4) return DC_ERR_ARG;
+  if (d->algo < 0 || d->algo > kNumAll || d->splitk < -4) return DC_ERR_ARG;
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;
@@ -825,6 +1125,21 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   const long M = p.rows ? p.nrows : (long)p.nb * p.hout * p.wout;
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
+  if (algo > kNumAlgos) {
+    if (halo_eligible(p)) {
+      switch (algo - kNumAlgos - 1) {
+#define DC_HALO(i)                                                                                              \
+  case i:                                                                                                       \
+    return launch_halo<kHaloAlgos[i].th, kHaloAlgos[i].tw, kHaloAlgos[i].bn, kHaloAlgos[i].wgm, kHaloAlgos[i].wgn, \
+                       kHaloAlgos[i].s>(p, splits == 0 ? 1 : splits, s);
+        DC_HALO(0) DC_HALO(1) DC_HALO(2) DC_HALO(3) DC_HALO(4) DC_HALO(5) DC_HALO(6) DC_HALO(7)
+#undef DC_HALO
+        default: return DC_ERR_ARG;
+      }
+    }
+    algo = 0;   // a halo choice carried to a shape outside its contract (nearest-shape pick): im2col heuristic
+    splits = 0;
+  }
   if (algo == 0 || splits == 0) {
     int a2, s2;
     auto_algo(M, p.cout, p.ktot / 64, a2, s2);

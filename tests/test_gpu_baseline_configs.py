@@ -107,8 +107,14 @@ def test_c2_teacher_forced_per_step(full_c2):
     HIP step and the bf16 oracle step both start from the fp32 oracle's state entering that step (latent, image
     latents, Adam state of the latent and of the learned affine, step counter) and are compared with the fp32
     oracle's step on v (UNet output), the latent gradient after the ||eps|| / ||g|| rescale, and the latent after
-    Adam + the DDIM update (marigold_dc.py:807-904).  Bounds (relative L2 over the frame, every step): v <= 1e-2,
-    gradient <= 2x the bf16 oracle's own error + 2e-2, new latent <= 2x the bf16 oracle's own error + 2e-3."""
+    Adam + the DDIM update (marigold_dc.py:807-904).
+
+    Measured on MI355X (profiles/r03b/c2_teacher_forced.txt), relative L2 over the frame: v 1.37-1.62 % (bf16
+    oracle 1.51-1.87 %), new latent 0.39-2.91 % (bf16 oracle 0.40-2.91 %; 2.9 % at t = 999, where Adam's first
+    step moves every element by +-lr on the sign of the gradient), gradient 25-55 % (bf16 oracle 26-76 %: the
+    point-loss gradient through a bf16 UNet backward is itself that noisy).  Bounds, every step: v <= 2 % and
+    <= 1.25x the bf16 oracle's + 1e-3; new latent <= 3.5 % and <= 1.25x the bf16 oracle's + 1e-3; gradient
+    <= 2x the bf16 oracle's + 2e-2."""
     from depth_completion_amd.config import MARIGOLD_V1
     from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
     f = full_c2
@@ -168,9 +174,9 @@ def test_c2_teacher_forced_per_step(full_c2):
     print(f"worst over 50 steps: v {worst[0]:.5f} ({worst_b[0]:.5f}) grad {worst[1]:.5f} ({worst_b[1]:.5f}) "
           f"latent {worst[2]:.5f} ({worst_b[2]:.5f})")
     for i, t, e, eb in rows:
-        assert e[0] <= 1e-2, (i, t, e, eb)
+        assert e[0] <= 0.02 and e[0] <= 1.25 * eb[0] + 1e-3, (i, t, e, eb)
         assert e[1] <= 2 * eb[1] + 2e-2, (i, t, e, eb)
-        assert e[2] <= 2 * eb[2] + 2e-3, (i, t, e, eb)
+        assert e[2] <= 0.035 and e[2] <= 1.25 * eb[2] + 1e-3, (i, t, e, eb)
 
 
 def test_c2_full_unet_50_steps(full_c2):
@@ -185,10 +191,13 @@ def test_c2_full_unet_50_steps(full_c2):
     print(f"\nC2 (full UNet, 768x576, 500 pts, 50 steps): HIP fitted |d| mean {mean_h:.5f} p99 {p99_h:.5f} "
           f"latent {lat_h:.4f} | oracle-bf16 mean {mean_b:.5f} p99 {p99_b:.5f} latent {lat_b:.4f}")
     # 50 chained bf16 Adam + DDIM steps on synthetic weights: the reference's own bf16 execution drifts from
-    # its fp32 one by ~3.7 % mean / 14 % p99 of the range here (chaotic guidance: Adam's first steps move
-    # every latent by +-lr on the sign of a gradient near zero), so the bound is relative to that drift; the
-    # absolute 2 % / 8 % bound is asserted at 10 steps (C1) where the bf16 oracle sits well inside it
+    # its fp32 one by 3.86 % mean / 14.5 % p99 of the range here (chaotic guidance: Adam's first steps move
+    # every latent by +-lr on the sign of a gradient near zero); per step the HIP path is as close to the fp32
+    # oracle as the bf16 oracle is (test_c2_teacher_forced_per_step).  Bounds: relative to that drift, and the
+    # stated absolute C2 tolerance -- fitted per-pixel |depth diff| <= 5 % mean / 19 % p99 of the frame's depth
+    # range (measured HIP 3.91 % / 14.8 %, profiles/r03b/; ~28 % headroom)
     assert mean_h <= 2 * mean_b + 1e-3 and p99_h <= 2 * p99_b + 1e-3
+    assert mean_h <= 0.05 and p99_h <= 0.19
     assert lat_h <= 2 * lat_b + 2e-3
 
 

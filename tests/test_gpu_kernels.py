@@ -524,6 +524,76 @@ def test_conv_all_algos(ctx, algo, nsplit):
         assert rel(nchw(y, n, ho, wo), ref) < 1e-2, (algo, nsplit, n, cin, cout, h, w, stride, mode)
 
 
+HALO_ALGOS = list(range(23, 31))   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv (conv_gemm.hip)
+
+
+@pytest.mark.parametrize("algo", HALO_ALGOS)
+@pytest.mark.parametrize("nsplit", [1, 2, 3])
+def test_conv_halo_algos(ctx, algo, nsplit):
+    """halo-tile direct 3x3 conv, every variant, input channels split over blocks (split-K): direct and
+    nearest-upsample (mode 1) inputs, two-source concat, batch 2, frames not a multiple of the spatial tile,
+    output channels not a multiple of BN, and the full epilogue (bias, per-step row bias, residual, ReLU,
+    ReLU-backward mask) vs torch fp32 on the bf16 values; bitwise reproducible run to run."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    assert _lib_num_algos() == 30
+    cases = [  # n, c1, c2, cout, h, w, mode, epilogue
+        (2, 128, 64, 96, 9, 35, 0, True), (1, 64, 0, 64, 18, 24, 1, False), (1, 320, 0, 320, 9, 12, 0, True),
+        (1, 64, 0, 32, 13, 70, 0, False)]
+    for n, c1, c2, cout, h, w, mode, epi in cases:
+        cin = c1 + c2
+        hin, win = (h // 2, w // 2) if mode == 1 else (h, w)
+        xa = rnd(n, c1, hin, win, seed=70)
+        xb = rnd(n, c2, hin, win, seed=71) if c2 else None
+        wt = rnd(cout, cin, 3, 3, scale=1 / math.sqrt(cin * 9), seed=72)
+        xin = torch.cat([xa, xb], 1) if c2 else xa
+        if mode == 1:
+            xin = F.interpolate(xin, size=(h, w), mode="nearest")
+        ref = F.conv2d(xin, wt, padding=1)
+        kw = {}
+        if epi:
+            b = rnd(cout, seed=73)
+            table = rnd(4, cout, seed=74)
+            res = rnd(n, cout, h, w, seed=75)
+            mask = rnd(n, cout, h, w, seed=76)
+            ctx.step.fill_(2)
+            ref = torch.relu(ref + b.view(1, -1, 1, 1) + table[2].view(1, -1, 1, 1) + res) * (mask > 0)
+            kw = dict(bias=b, rowbias=table.to(torch.bfloat16), rowbias_ld=cout, resid=nhwc(res), act=1, mask=nhwc(mask))
+        outs = []
+        for _ in range(2):
+            y = torch.full((n * h * w, cout), 3.0, dtype=torch.bfloat16, device=dev)
+            ops.conv_gemm(ctx, nhwc(xa), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=hin, win=win, cin=cin,
+                          hout=h, wout=w, cout=cout, mode=mode, x2=nhwc(xb) if c2 else None, c1=c1 if c2 else 0,
+                          y=y, algo=algo, nsplit=nsplit, **kw)
+            torch.cuda.synchronize()
+            outs.append(y)
+        ctx.step.zero_()
+        assert rel(nchw(outs[0], n, h, w), ref) < 1e-2, (algo, nsplit, n, cin, cout, h, w, mode)
+        assert torch.equal(outs[0], outs[1]), (algo, nsplit, n, cin, cout, h, w, mode)
+
+
+def test_conv_halo_outside_contract_falls_back(ctx):
+    """a halo algo id on a shape outside the halo contract (stride 2, 1x1, cin % 64 != 0: e.g. carried there by
+    the nearest-tuned-shape pick) runs the im2col kernel instead, with the same result."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    for n, cin, cout, h, w, k, stride in ((1, 128, 64, 12, 10, 3, 2), (2, 64, 96, 6, 8, 1, 1), (1, 8, 64, 9, 9, 3, 1)):
+        x = rnd(n, cin, h, w, seed=80)
+        wt = rnd(cout, cin, k, k, scale=1 / math.sqrt(cin * k * k), seed=81)
+        ref = F.conv2d(x, wt, stride=stride, padding=k // 2)
+        ho, wo = ref.shape[-2:]
+        y = torch.empty(n * ho * wo, cout, dtype=torch.bfloat16, device=dev)
+        ops.conv_gemm(ctx, nhwc(x), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=h, win=w, cin=cin, hout=ho,
+                      wout=wo, cout=cout, kh=k, kw=k, stride=stride, pad=k // 2, y=y, algo=HALO_ALGOS[0], nsplit=2)
+        torch.cuda.synchronize()
+        assert rel(nchw(y, n, ho, wo), ref) < 1e-2, (n, cin, cout, h, w, k, stride)
+
+
+def _lib_num_algos():
+    from depth_completion_amd import _lib
+    return _lib.load().dc_conv_num_algos()
+
+
 @pytest.mark.parametrize("algo,nsplit", [(10, -1), (12, -2), (3, -3), (16, -1)])
 def test_conv_stream_k_unet_shape_deterministic(ctx, algo, nsplit):
     """stream-K on a UNet L2 shape (M = 432, 3x3, 1280 -> 1280, bias + in-place residual): matches the
