@@ -131,12 +131,19 @@ def pick_variant(table: list, key: tuple) -> tuple:
     return (out[0], out[1])
 
 
-def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin: int, hout: int, wout: int,
+def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, y=None, **kw):
+    """rows: optional (int32 tensor, count) -- compute only those output pixels (sorted row indices)."""
+    d = conv_desc(ctx, x, w, y=y, **kw)
+    call("dc_conv_gemm", C.byref(d), ctx.stream)
+    return y
+
+
+def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin: int, hout: int, wout: int,
               cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
               c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
               y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None, geglu: int = 0,
               y2=None, aux=None, rows=None):
-    """rows: optional (int32 tensor, count) -- compute only those output pixels (sorted row indices)."""
+    """The dc_conv_desc of one conv_gemm call, its (algo, split) chosen (tuned table / nearest shape)."""
     d = ConvDesc()
     d.x = P(x)
     d.ldx = LD(x)
@@ -174,8 +181,7 @@ def conv_gemm(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
         algo, nsplit = ctx.choose_algo(d, y, srcs=(x, x2, resid))
     d.algo = algo
     d.splitk = nsplit or 0
-    call("dc_conv_gemm", C.byref(d), ctx.stream)
-    return y
+    return d
 
 
 def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
