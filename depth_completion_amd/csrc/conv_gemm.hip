@@ -725,27 +725,24 @@ struct HaloCfg {
   static constexpr int RING = 2 * HALO + S * WST;
   static constexpr int EPI = 4 * WM * (WN + 8) * 2;
   static constexpr int LDS = RING > EPI ? RING : EPI;
-  static_assert(S >= 2 && S <= 8, "ring depth");
+  static_assert(S >= 2 && S <= 16, "ring depth");
   static_assert((S - 2) * LW + LH <= 63, "vmcnt range");
 };
 
 // wait until at most k weight slices (+ e halos) issued after the current iteration's loads are in flight
-template <int LW, int LH, int S>
+// (k <= K; the vmcnt immediate is selected by a compile-time chain)
+template <int LW, int LH, int K>
 __device__ __forceinline__ void halo_wait(int k, int e) {
-#define DC_HW(K)                                           \
-  if (k == K) {                                            \
-    if (e) vm_wait<(K) * LW + ((K) > 0 ? LH : 0)>();       \
-    else vm_wait<(K) * LW>();                              \
-    return;                                                \
+  if constexpr (K == 0) {
+    vm_wait<0>();
+  } else {
+    if (k == K) {
+      if (e) vm_wait<K * LW + LH>();
+      else vm_wait<K * LW>();
+      return;
+    }
+    halo_wait<LW, LH, K - 1>(k, e);
   }
-  if constexpr (S >= 8) { DC_HW(6) }
-  if constexpr (S >= 7) { DC_HW(5) }
-  if constexpr (S >= 6) { DC_HW(4) }
-  if constexpr (S >= 5) { DC_HW(3) }
-  if constexpr (S >= 4) { DC_HW(2) }
-  if constexpr (S >= 3) { DC_HW(1) }
-  vm_wait<0>();
-#undef DC_HW
 }
 
 template <int TH, int TW, int BN, int WGM, int WGN, int S>
@@ -856,7 +853,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) 
     const int last = min(i + S - 2, NI - 1);
     const int k = last - i;
     const int e = (k > 0 && (tap + k) >= 9) ? 1 : 0;
-    halo_wait<LW, LH, S>(k, e);
+    halo_wait<LW, LH, S - 2>(k, e);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -936,14 +933,19 @@ struct HaloAlgo {
   int th, tw, bn, wgm, wgn, s;
 };
 constexpr HaloAlgo kHaloAlgos[] = {
-    {8, 32, 64, 4, 1, 4},   // 256 px x 64: TAESD 64-channel levels, UNet level 0
-    {4, 32, 64, 2, 2, 3},   // 128 px x 64 at 2 blocks / CU
-    {4, 32, 32, 4, 1, 4},   // 128 px x 32
-    {8, 16, 64, 4, 1, 4},   // 128 px x 64, 16 wide (level 1: 48 columns)
-    {6, 24, 64, 1, 4, 4},   // 144 px x 64 (level 2: 18 x 24)
-    {9, 12, 64, 1, 4, 4},   // 108 px x 64 (level 3: 9 x 12, the whole frame)
-    {9, 12, 32, 2, 2, 4},   // 108 px x 32 (level 3)
-    {8, 24, 32, 2, 2, 4},   // 192 px x 32 (level 2)
+    // deep weight rings at one block per CU: the fill is bound by the bytes a CU keeps in flight (~1 us
+    // issue-to-landed under load), so the ring holds 7-15 (tap, chunk) slices
+    {8, 32, 64, 4, 1, 8},    // 256 px x 64, 152 KB
+    {4, 32, 64, 2, 2, 12},   // 128 px x 64, 152 KB
+    {4, 32, 32, 4, 1, 16},   // 128 px x 32, 120 KB
+    {8, 16, 64, 4, 1, 12},   // 128 px x 64, 16 wide (level 1: 48 columns), 144 KB
+    {6, 24, 64, 1, 4, 12},   // 144 px x 64 (level 2: 18 x 24), 152 KB
+    {9, 12, 64, 1, 4, 14},   // 108 px x 64 (level 3: the whole 9 x 12 frame), 152 KB
+    {9, 12, 32, 2, 2, 16},   // 108 px x 32 (level 3), 104 KB
+    {8, 24, 32, 2, 2, 16},   // 192 px x 32 (level 2), 136 KB
+    // two blocks per CU (<= 80 KB)
+    {8, 16, 64, 4, 1, 4},    // 128 px x 64
+    {4, 32, 64, 2, 2, 3},    // 128 px x 64
 };
 
 constexpr long kCounterBytes = 64 * 1024;
@@ -964,7 +966,7 @@ constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 
 constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
 constexpr int kNumHalo = sizeof(kHaloAlgos) / sizeof(kHaloAlgos[0]);
 constexpr int kNumAll = kNumAlgos + kNumHalo;   // algo ids kNumAlgos + 1 .. kNumAll: halo variants
-static_assert(kNumHalo == 8, "DC_HALO cases below");
+static_assert(kNumHalo == 10, "DC_HALO cases below");
 
 template <int TH, int TW, int BN, int WGM, int WGN, int S>
 int launch_halo(ConvGemmParams& p, int splits, hipStream_t stream) {
@@ -1132,7 +1134,8 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   case i:                                                                                                       \
     return launch_halo<kHaloAlgos[i].th, kHaloAlgos[i].tw, kHaloAlgos[i].bn, kHaloAlgos[i].wgm, kHaloAlgos[i].wgn, \
                        kHaloAlgos[i].s>(p, splits == 0 ? 1 : splits, s);
-        DC_HALO(0) DC_HALO(1) DC_HALO(2) DC_HALO(3) DC_HALO(4) DC_HALO(5) DC_HALO(6) DC_HALO(7)
+        DC_HALO(0) DC_HALO(1) DC_HALO(2) DC_HALO(3) DC_HALO(4) DC_HALO(5) DC_HALO(6) DC_HALO(7) DC_HALO(8)
+        DC_HALO(9)
 #undef DC_HALO
         default: return DC_ERR_ARG;
       }
