@@ -722,11 +722,14 @@ struct HaloCfg {
   static constexpr int RB = 128;                 // 64 bf16 channels per LDS row
   static constexpr int HALO = LH * 32 * RB;
   static constexpr int WST = BN * RB;
-  static constexpr int RING = 2 * HALO + S * WST;
+  // halo slots: chunk c's halo is issued S - 1 iterations ahead of its tap 0, into the slot chunk c - NH used,
+  // whose last read (its tap 8) must precede that issue: S <= 9 NH - 8
+  static constexpr int NH = S <= 10 ? 2 : 3;
+  static constexpr int RING = NH * HALO + S * WST;
   static constexpr int EPI = 4 * WM * (WN + 8) * 2;
   static constexpr int LDS = RING > EPI ? RING : EPI;
-  static_assert(S >= 2 && S <= 16, "ring depth");
-  static_assert((S - 2) * LW + LH <= 63, "vmcnt range");
+  static_assert(S >= 2 && S <= 19, "ring depth (three halo slots)");
+  static_assert((S - 2) * LW + (S >= 12 ? 2 : 1) * LH <= 63, "vmcnt range");
 };
 
 // wait until at most k weight slices (+ e halos) issued after the current iteration's loads are in flight
@@ -737,7 +740,8 @@ __device__ __forceinline__ void halo_wait(int k, int e) {
     vm_wait<0>();
   } else {
     if (k == K) {
-      if (e) vm_wait<K * LW + LH>();
+      if (e == 2) vm_wait<K * LW + (K >= 10 ? 2 * LH : LH)>();
+      else if (e == 1) vm_wait<K * LW + LH>();
       else vm_wait<K * LW>();
       return;
     }
@@ -818,7 +822,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) 
   int q_c = c_begin, q_t = 0;
   auto issue = [&]() __attribute__((always_inline)) {
     if (q_t == 0) {
-      DC_LDS char* hb = (DC_LDS char*)smem + ((q_c - c_begin) & 1) * C::HALO;
+      DC_LDS char* hb = (DC_LDS char*)smem + ((q_c - c_begin) % C::NH) * C::HALO;
       const int ch = q_c * 64;
       if (ch >= p.c1) {
 #pragma unroll
@@ -828,7 +832,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) 
         for (int j = 0; j < LH; ++j) buf_load_lds16(ra, hb + (wid_s * 64 + 256 * j) * 16, h_off[j], ch * 2);
       }
     }
-    DC_LDS char* wb = (DC_LDS char*)smem + 2 * C::HALO + (q_i % S) * C::WST;
+    DC_LDS char* wb = (DC_LDS char*)smem + C::NH * C::HALO + (q_i % S) * C::WST;
     const int koff = (q_t * p.cin + q_c * 64) * 2;
 #pragma unroll
     for (int j = 0; j < LW; ++j) buf_load_lds16(rb, wb + (wid_s * 64 + 256 * j) * 16, b_off[j], koff);
@@ -849,17 +853,17 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) 
   for (int s = 0; s < S - 1 && s < NI; ++s) issue();
   int tap = 0, cpar = 0;
   for (int i = 0; i < NI; ++i) {
-    // loads younger than iteration i's: iterations i+1 .. min(i+S-2, NI-1); one of them may carry a halo
+    // loads younger than iteration i's: iterations i+1 .. min(i+S-2, NI-1); e of them carry a halo (tap 0)
     const int last = min(i + S - 2, NI - 1);
     const int k = last - i;
-    const int e = (k > 0 && (tap + k) >= 9) ? 1 : 0;
+    const int e = (tap + k) >= 18 ? 2 : ((tap + k) >= 9 ? 1 : 0);
     halo_wait<LW, LH, S - 2>(k, e);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (i + S - 1 < NI) issue();
     const char* ha = smem + cpar * C::HALO;
-    const char* wbase = smem + 2 * C::HALO + (i % S) * C::WST;
+    const char* wbase = smem + C::NH * C::HALO + (i % S) * C::WST;
     const int ky = tap >= 6 ? 2 : (tap >= 3 ? 1 : 0);
     const int toff = ky * C::HW2 + (tap - 3 * ky);
     bf16x8 af[2][MI], bfr[2][NJ];
@@ -888,7 +892,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) 
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
     if (++tap == 9) {
       tap = 0;
-      cpar ^= 1;
+      cpar = cpar + 1 == C::NH ? 0 : cpar + 1;
     }
   }
   vm_wait<0>();
@@ -936,13 +940,13 @@ constexpr HaloAlgo kHaloAlgos[] = {
     // deep weight rings at one block per CU: the fill is bound by the bytes a CU keeps in flight (~1 us
     // issue-to-landed under load), so the ring holds 7-15 (tap, chunk) slices
     {8, 32, 64, 4, 1, 8},    // 256 px x 64, 152 KB
-    {4, 32, 64, 2, 2, 12},   // 128 px x 64, 152 KB
-    {4, 32, 32, 4, 1, 16},   // 128 px x 32, 120 KB
-    {8, 16, 64, 4, 1, 12},   // 128 px x 64, 16 wide (level 1: 48 columns), 144 KB
-    {6, 24, 64, 1, 4, 12},   // 144 px x 64 (level 2: 18 x 24), 152 KB
-    {9, 12, 64, 1, 4, 14},   // 108 px x 64 (level 3: the whole 9 x 12 frame), 152 KB
-    {9, 12, 32, 2, 2, 16},   // 108 px x 32 (level 3), 104 KB
-    {8, 24, 32, 2, 2, 16},   // 192 px x 32 (level 2), 136 KB
+    {4, 32, 64, 2, 2, 10},   // 128 px x 64, 136 KB
+    {4, 32, 32, 4, 1, 16},   // 128 px x 32, three halo slots, 148 KB
+    {8, 16, 64, 4, 1, 10},   // 128 px x 64, 16 wide (level 1: 48 columns), 128 KB
+    {6, 24, 64, 1, 4, 10},   // 144 px x 64 (level 2: 18 x 24), 136 KB
+    {9, 12, 64, 1, 4, 12},   // 108 px x 64 (level 3: the whole 9 x 12 frame), three halo slots, 156 KB
+    {9, 12, 32, 2, 2, 16},   // 108 px x 32 (level 3), three halo slots, 124 KB
+    {8, 24, 32, 2, 2, 13},   // 192 px x 32 (level 2), three halo slots, 160 KB
     // two blocks per CU (<= 80 KB)
     {8, 16, 64, 4, 1, 4},    // 128 px x 64
     {4, 32, 64, 2, 2, 3},    // 128 px x 64
