@@ -17,6 +17,7 @@
 // iteration space per block); a tile computed in pieces is summed in piece order by its
 // last-arriving block (deterministic, no second kernel).
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 #include "../../include/dcamd.h"
@@ -54,6 +55,8 @@ struct ConvGemmParams {
   int ldaux;
   const int* rows;      // optional: GEMM row m computes output pixel rows[m] (sorted), nrows of them
   long nrows;
+  int diag;             // halo kernel diagnostics (env DC_HALO_DIAG, experiments only): 1 no LDS-DMA, 2 no MFMA
+                        // / fragment reads, 4 no barrier
   int nmajor;           // tile order within an XCD's range: 0 M-major (row tiles share A), 1 N-major (column
                         // tiles share W; opt-in, DC_GEMM_ORDER=2)
   // multiply-shift division by hout * wout, wout and hout (fast_div): the pixel -> (frame, y, x) split of
@@ -722,157 +725,93 @@ struct HaloCfg {
   static constexpr int RB = 128;                 // 64 bf16 channels per LDS row
   static constexpr int HALO = LH * 32 * RB;
   static constexpr int WST = BN * RB;
-  // halo slots: chunk c's halo is issued S - 1 iterations ahead of its tap 0, into the slot chunk c - NH used,
-  // whose last read (its tap 8) must precede that issue: S <= 9 NH - 8
-  static constexpr int NH = S <= 10 ? 2 : 3;
-  static constexpr int RING = NH * HALO + S * WST;
+  // two halo slots: chunk c's halo is issued S - 1 iterations ahead of its tap 0, into the slot chunk c - 2
+  // used, whose last read (its tap 8) precedes that issue for S <= 10
+  static constexpr int RING = 2 * HALO + S * WST;
   static constexpr int EPI = 4 * WM * (WN + 8) * 2;
   static constexpr int LDS = RING > EPI ? RING : EPI;
-  static_assert(S >= 2 && S <= 19, "ring depth (three halo slots)");
-  static_assert((S - 2) * LW + (S >= 12 ? 2 : 1) * LH <= 63, "vmcnt range");
+  static_assert(S >= 2 && S <= 10, "ring depth (two halo slots)");
+  static_assert((S - 2) * LW + LH <= 63, "vmcnt range");
 };
 
-// wait until at most k weight slices (+ e halos) issued after the current iteration's loads are in flight
-// (k <= K; the vmcnt immediate is selected by a compile-time chain)
-template <int LW, int LH, int K>
-__device__ __forceinline__ void halo_wait(int k, int e) {
-  if constexpr (K == 0) {
-    vm_wait<0>();
-  } else {
-    if (k == K) {
-      if (e == 2) vm_wait<K * LW + (K >= 10 ? 2 * LH : LH)>();
-      else if (e == 1) vm_wait<K * LW + LH>();
-      else vm_wait<K * LW>();
-      return;
-    }
-    halo_wait<LW, LH, K - 1>(k, e);
-  }
-}
-
+// The main loop is unrolled over the 9 taps of a chunk, so every count below is a compile-time constant: at tap t
+// of a chunk that is not the block's last, the loads younger than iteration i's are iterations i+1 .. i+S-2,
+// (S-2) LW weight pieces plus one halo when t + S - 2 >= 9; in the last chunk only min(S-2, 8-t) iterations
+// follow, none with a halo.  (A runtime-selected vmcnt was a ~450-cycle branch chain per iteration.)
 template <int TH, int TW, int BN, int WGM, int WGN, int S>
-__global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) {
+struct HaloBlock {
   using C = HaloCfg<TH, TW, BN, WGM, WGN, S>;
-  constexpr int MI = C::MI, NJ = C::NJ, WM = C::WM, WN = C::WN, RB = C::RB, LH = C::LH, LW = C::LW;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
-  const int wm = wid / WGN, wn = wid % WGN;
+  static constexpr int MI = C::MI, NJ = C::NJ, WM = C::WM, WN = C::WN, RB = C::RB, LH = C::LH, LW = C::LW;
+  static_assert(S <= 10, "two halo slots: the unrolled schedule assumes S - 1 <= 9");
+  static constexpr int kOOB = (int)0x80000000u;
 
-  // ---- block -> (split, column tile, frame, tile row, tile column): split-major over the whole grid
-  const int tiles_n = (p.cout + BN - 1) / BN;
-  const int tiles_x = (p.wout + TW - 1) / TW, tiles_y = (p.hout + TH - 1) / TH;
-  const int tiles = gridDim.x, nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
-  const int wk = xcd_remap(bid, nblk);
-  const int split = wk / tiles;
-  const int lb = wk - split * tiles;
-  const int sp_tile = lb / tiles_n, tn = lb - (lb / tiles_n) * tiles_n;
-  const int frame = sp_tile / (tiles_y * tiles_x);
-  const int trem = sp_tile - frame * (tiles_y * tiles_x);
-  const int oy0 = (trem / tiles_x) * TH, ox0 = (trem - (trem / tiles_x) * tiles_x) * TW;
-  const int n0 = tn * BN;
-  const int nck = p.cin / 64;
-  const int c_begin = split * p.kps;
-  const int c_end = min(nck, c_begin + p.kps);
-  const int NI = max(0, c_end - c_begin) * 9;
+  const ConvGemmParams& p;
+  char* smem;
+  int lane, wid_s, wm, wn;
+  int frame, oy0, ox0, n0, c_begin, c_end;
+  int h_off[LH], h_off2[LH], b_off[LW], hbase[MI];
+  __amdgpu_buffer_rsrc_t ra, ra2, rb;
+  // issue cursor (scalar): the next iteration to load (its chunk, tap and weight slot)
+  int q_c, q_t, q_slot;
+  // compute cursor: the current chunk's halo slot and the current weight slot
+  int cpar, wslot;
+  f32x4 acc[MI][NJ];
 
-  // ---- per-lane LDS-DMA offsets: halo rows (fixed for the block; the chunk's channel offset rides in soffset)
-  constexpr int kOOB = (int)0x80000000u;
-  const int slot = tid & 7, r0 = tid >> 3;
-  const bool two_src = p.c1 < p.cin;
-  int h_off[LH], h_off2[LH];
+  __device__ __forceinline__ void issue_halo(int c) {
+    DC_LDS char* hb = (DC_LDS char*)smem + ((c - c_begin) & 1) * C::HALO;
+    const int ch = c * 64;
+    if (ch >= p.c1) {
 #pragma unroll
-  for (int j = 0; j < LH; ++j) {
-    const int hr = r0 + 32 * j;
-    const int hy = hr / C::HW2, hx = hr - (hr / C::HW2) * C::HW2;
-    const int vy = oy0 - 1 + hy, vx = ox0 - 1 + hx;
-    bool ok = hr < C::HROWS && vy >= 0 && vy < p.hout && vx >= 0 && vx < p.wout;
-    int iy = vy, ix = vx;
-    if (p.mode == 1) {
-      iy = ok ? (int)fast_div((unsigned)(vy * p.hin), p.h_mul, p.h_shr) : 0;
-      ix = ok ? (int)fast_div((unsigned)(vx * p.win), p.w_mul, p.w_shr) : 0;
+      for (int j = 0; j < LH; ++j) buf_load_lds16(ra2, hb + (wid_s * 64 + 256 * j) * 16, h_off2[j], (ch - p.c1) * 2);
+    } else {
+#pragma unroll
+      for (int j = 0; j < LH; ++j) buf_load_lds16(ra, hb + (wid_s * 64 + 256 * j) * 16, h_off[j], ch * 2);
     }
-    const int pix = (frame * p.hin + iy) * p.win + ix;
-    const int sw = (slot ^ (hr & 7)) * 8;
-    h_off[j] = ok ? (pix * p.ldx + sw) * 2 : kOOB;
-    h_off2[j] = ok ? (pix * p.ldx2 + sw) * 2 : kOOB;
   }
-  int b_off[LW];
-#pragma unroll
-  for (int j = 0; j < LW; ++j) {
-    const int row = r0 + 32 * j;
-    const int co = n0 + row;
-    b_off[j] = co < p.cout ? (co * p.ktot + (slot ^ (row & 7)) * 8) * 2 : kOOB;
-  }
-  const __amdgpu_buffer_rsrc_t ra = buf_rsrc(p.x);
-  const __amdgpu_buffer_rsrc_t ra2 = buf_rsrc(p.x2);
-  const __amdgpu_buffer_rsrc_t rb = buf_rsrc(p.w);
-
-  // per-lane halo row of each A fragment at tap (0, 0)
-  int hbase[MI];
-#pragma unroll
-  for (int ii = 0; ii < MI; ++ii) {
-    int pl = wm * WM + ii * 16 + (lane & 15);
-    pl = pl < C::BM ? pl : 0;   // pad rows read a valid halo row; never stored
-    const int ty = pl / TW, tx = pl - (pl / TW) * TW;
-    hbase[ii] = ty * C::HW2 + tx;
-  }
-
-  // issue cursor (scalar): next iteration's chunk / tap
-  int q_i = 0;
-  int q_c = c_begin, q_t = 0;
-  auto issue = [&]() __attribute__((always_inline)) {
-    if (q_t == 0) {
-      DC_LDS char* hb = (DC_LDS char*)smem + ((q_c - c_begin) % C::NH) * C::HALO;
-      const int ch = q_c * 64;
-      if (ch >= p.c1) {
-#pragma unroll
-        for (int j = 0; j < LH; ++j) buf_load_lds16(ra2, hb + (wid_s * 64 + 256 * j) * 16, h_off2[j], (ch - p.c1) * 2);
-      } else {
-#pragma unroll
-        for (int j = 0; j < LH; ++j) buf_load_lds16(ra, hb + (wid_s * 64 + 256 * j) * 16, h_off[j], ch * 2);
-      }
-    }
-    DC_LDS char* wb = (DC_LDS char*)smem + C::NH * C::HALO + (q_i % S) * C::WST;
-    const int koff = (q_t * p.cin + q_c * 64) * 2;
+  __device__ __forceinline__ void issue_w(int c, int t) {
+    DC_LDS char* wb = (DC_LDS char*)smem + 2 * C::HALO + q_slot * C::WST;
+    const int koff = (t * p.cin + c * 64) * 2;
 #pragma unroll
     for (int j = 0; j < LW; ++j) buf_load_lds16(rb, wb + (wid_s * 64 + 256 * j) * 16, b_off[j], koff);
-    ++q_i;
+    q_slot = q_slot + 1 == S ? 0 : q_slot + 1;
+  }
+  // generic issue of the next iteration (prologue only)
+  __device__ __forceinline__ void issue_next() {
+    if (q_t == 0) issue_halo(q_c);
+    issue_w(q_c, q_t);
     if (++q_t == 9) {
       q_t = 0;
       ++q_c;
     }
-  };
-  (void)two_src;
+  }
 
-  f32x4 acc[MI][NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int s = 0; s < S - 1 && s < NI; ++s) issue();
-  int tap = 0, cpar = 0;
-  for (int i = 0; i < NI; ++i) {
-    // loads younger than iteration i's: iterations i+1 .. min(i+S-2, NI-1); e of them carry a halo (tap 0)
-    const int last = min(i + S - 2, NI - 1);
-    const int k = last - i;
-    const int e = (tap + k) >= 18 ? 2 : ((tap + k) >= 9 ? 1 : 0);
-    halo_wait<LW, LH, S - 2>(k, e);
+  // one iteration (chunk c = current, tap T)
+  template <int T, bool LAST>
+  __device__ __forceinline__ void tap_step() {
+    constexpr int K = LAST ? ((S - 2) < (8 - T) ? (S - 2) : (8 - T)) : (S - 2);
+    constexpr int E = (!LAST && T + S - 2 >= 9) ? 1 : 0;
+    vm_wait<K * LW + E * LH>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (i + S - 1 < NI) issue();
+    // load iteration i + S - 1: chunk + (T + S - 1 >= 9), tap (T + S - 1) % 9 (none past the block's last)
+    constexpr int TT = T + S - 1;
+    if constexpr (!LAST || TT < 9) {
+      if constexpr (TT % 9 == 0) issue_halo(q_c);
+      issue_w(q_c, TT % 9);
+      if constexpr (TT % 9 == 8) ++q_c;
+    }
+    constexpr int KY = T / 3, KX = T % 3;
+    constexpr int TOFF = KY * C::HW2 + KX;
     const char* ha = smem + cpar * C::HALO;
-    const char* wbase = smem + C::NH * C::HALO + (i % S) * C::WST;
-    const int ky = tap >= 6 ? 2 : (tap >= 3 ? 1 : 0);
-    const int toff = ky * C::HW2 + (tap - 3 * ky);
+    const char* wbase = smem + 2 * C::HALO + wslot * C::WST;
     bf16x8 af[2][MI], bfr[2][NJ];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int ii = 0; ii < MI; ++ii) {
-        const int r = hbase[ii] + toff;
+        const int r = hbase[ii] + TOFF;
         af[ks][ii] = *reinterpret_cast<const bf16x8*>(ha + r * RB + ((chunk ^ (r & 7)) << 4));
       }
 #pragma unroll
@@ -890,46 +829,141 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) 
           acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][ii], bfr[ks][jj], acc[ii][jj], 0, 0, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
-    if (++tap == 9) {
-      tap = 0;
-      cpar = cpar + 1 == C::NH ? 0 : cpar + 1;
-    }
+    wslot = wslot + 1 == S ? 0 : wslot + 1;
   }
-  vm_wait<0>();
+  template <bool LAST, int... T>
+  __device__ __forceinline__ void chunk_steps(std::integer_sequence<int, T...>) {
+    (tap_step<T, LAST>(), ...);
+  }
 
-  if (p.splits > 1 &&
-      !tile_handoff_g<MI, NJ>(p, smem, lb, split * tiles + lb, p.splits, [&](int sp) { return sp * tiles + lb; }, acc))
-    return;
+  __device__ __forceinline__ void run() {
+    const int tid = threadIdx.x;
+    lane = tid & 63;
+    wid_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    wm = (tid >> 6) / WGN;
+    wn = (tid >> 6) % WGN;
+    // ---- block -> (split, column tile, frame, tile row, tile column): split-major over the whole grid
+    const int tiles_n = (p.cout + BN - 1) / BN;
+    const int tiles_x = (p.wout + TW - 1) / TW, tiles_y = (p.hout + TH - 1) / TH;
+    const int tiles = gridDim.x, nblk = gridDim.x * gridDim.y, bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int wk = xcd_remap(bid, nblk);
+    const int split = wk / tiles;
+    const int lb = wk - split * tiles;
+    const int sp_tile = lb / tiles_n, tn = lb - (lb / tiles_n) * tiles_n;
+    frame = sp_tile / (tiles_y * tiles_x);
+    const int trem = sp_tile - frame * (tiles_y * tiles_x);
+    oy0 = (trem / tiles_x) * TH;
+    ox0 = (trem - (trem / tiles_x) * tiles_x) * TW;
+    n0 = tn * BN;
+    const int nck = p.cin / 64;
+    c_begin = split * p.kps;
+    c_end = min(nck, c_begin + p.kps);
+    const int nch = max(0, c_end - c_begin);
 
-  // ---- epilogue: bias in fp32, bf16 per-wave LDS tile, then 16-B rows mapped to the tile's output pixels
-  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  __syncthreads();
-  constexpr int LDE = WN + 8;
-  bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
+    // ---- per-lane LDS-DMA offsets: halo rows (fixed for the block; the chunk's channel offset rides in soffset)
+    const int slot = tid & 7, r0 = tid >> 3;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int c = n0 + wn * WN + j * 16 + col_l;
-    const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+    for (int j = 0; j < LH; ++j) {
+      const int hr = r0 + 32 * j;
+      const int hy = hr / C::HW2, hx = hr - (hr / C::HW2) * C::HW2;
+      const int vy = oy0 - 1 + hy, vx = ox0 - 1 + hx;
+      const bool ok = hr < C::HROWS && vy >= 0 && vy < p.hout && vx >= 0 && vx < p.wout;
+      int iy = vy, ix = vx;
+      if (p.mode == 1) {
+        iy = ok ? (int)fast_div((unsigned)(vy * p.hin), p.h_mul, p.h_shr) : 0;
+        ix = ok ? (int)fast_div((unsigned)(vx * p.win), p.w_mul, p.w_shr) : 0;
+      }
+      const int pix = (frame * p.hin + iy) * p.win + ix;
+      const int sw = (slot ^ (hr & 7)) * 8;
+      h_off[j] = ok ? (pix * p.ldx + sw) * 2 : kOOB;
+      h_off2[j] = ok ? (pix * p.ldx2 + sw) * 2 : kOOB;
+    }
+#pragma unroll
+    for (int j = 0; j < LW; ++j) {
+      const int row = r0 + 32 * j;
+      const int co = n0 + row;
+      b_off[j] = co < p.cout ? (co * p.ktot + (slot ^ (row & 7)) * 8) * 2 : kOOB;
+    }
+    ra = buf_rsrc(p.x);
+    ra2 = buf_rsrc(p.x2);
+    rb = buf_rsrc(p.w);
+    // per-lane halo row of each A fragment at tap (0, 0)
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii) {
+      int pl = wm * WM + ii * 16 + (lane & 15);
+      pl = pl < C::BM ? pl : 0;   // pad rows read a valid halo row; never stored
+      const int ty = pl / TW, tx = pl - (pl / TW) * TW;
+      hbase[ii] = ty * C::HW2 + tx;
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) es[(i * 16 + row_l + q) * LDE + j * 16 + col_l] = (bf16)(acc[i][j][q] + bv);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    q_c = c_begin;
+    q_t = 0;
+    q_slot = 0;
+    const int NI = nch * 9;
+    for (int s = 0; s < S - 1 && s < NI; ++s) issue_next();
+    // after the prologue the issue cursor sits at iteration S - 1: chunk c_begin + (S-1)/9 ... (S - 1 <= 9)
+    cpar = 0;
+    wslot = 0;
+    for (int c = 0; c < nch; ++c) {
+      // keep the 9 taps' fragment addresses out of registers across chunks (hoisted, they cost 9 x 2 x MI VGPRs
+      // and spilled the 9-fragment variants): recomputed per tap, in the MFMAs' VALU shadow
+#pragma unroll
+      for (int ii = 0; ii < MI; ++ii) asm volatile("" : "+v"(hbase[ii]));
+      if (c + 1 < nch) chunk_steps<false>(std::make_integer_sequence<int, 9>{});
+      else chunk_steps<true>(std::make_integer_sequence<int, 9>{});
+      cpar ^= 1;
+    }
+    vm_wait<0>();
+
+    if (p.splits > 1 && !tile_handoff_g<MI, NJ>(p, smem, lb, split * tiles + lb, p.splits,
+                                                [&](int sp) { return sp * tiles + lb; }, acc))
+      return;
+    epilogue();
   }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  constexpr int GPR = WN / 8;
+
+  // ---- epilogue: bias in fp32, bf16 per-wave LDS tile, then 16-B rows mapped to the tile's output pixels
+  __device__ __forceinline__ void epilogue() {
+    const int wid = threadIdx.x >> 6;
+    const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+    __syncthreads();
+    constexpr int LDE = WN + 8;
+    bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = n0 + wn * WN + j * 16 + col_l;
+      const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) es[(i * 16 + row_l + q) * LDE + j * 16 + col_l] = (bf16)(acc[i][j][q] + bv);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int GPR = WN / 8;
 #pragma unroll 4
-  for (int g = lane; g < WM * GPR; g += 64) {
-    const int row = g / GPR, cg = g - (g / GPR) * GPR;
-    const int pl = wm * WM + row;
-    const int c = n0 + wn * WN + cg * 8;
-    const int ty = pl / TW, tx = pl - (pl / TW) * TW;
-    const int oy = oy0 + ty, ox = ox0 + tx;
-    if (pl >= C::BM || oy >= p.hout || ox >= p.wout || c >= p.cout) continue;
-    float v[8];
-    load8(es + row * LDE + cg * 8, v);
-    epilogue_store(p, ((long)frame * p.hout + oy) * p.wout + ox, c, v, false);
+    for (int g = lane; g < WM * GPR; g += 64) {
+      const int row = g / GPR, cg = g - (g / GPR) * GPR;
+      const int pl = wm * WM + row;
+      const int c = n0 + wn * WN + cg * 8;
+      const int ty = pl / TW, tx = pl - (pl / TW) * TW;
+      const int oy = oy0 + ty, ox = ox0 + tx;
+      if (pl >= C::BM || oy >= p.hout || ox >= p.wout || c >= p.cout) continue;
+      float v[8];
+      load8(es + row * LDE + cg * 8, v);
+      epilogue_store(p, ((long)frame * p.hout + oy) * p.wout + ox, c, v, false);
+    }
   }
+};
+
+template <int TH, int TW, int BN, int WGM, int WGN, int S>
+__global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[HaloCfg<TH, TW, BN, WGM, WGN, S>::LDS];
+  HaloBlock<TH, TW, BN, WGM, WGN, S> blk{p, smem};
+  blk.run();
 }
 
 // halo variants: (TH, TW, BN, wave layout WGM x WGN, weight ring depth S)
@@ -937,16 +971,14 @@ struct HaloAlgo {
   int th, tw, bn, wgm, wgn, s;
 };
 constexpr HaloAlgo kHaloAlgos[] = {
-    // deep weight rings at one block per CU: the fill is bound by the bytes a CU keeps in flight (~1 us
-    // issue-to-landed under load), so the ring holds 7-15 (tap, chunk) slices
-    {8, 32, 64, 4, 1, 8},    // 256 px x 64, 152 KB
-    {4, 32, 64, 2, 2, 10},   // 128 px x 64, 136 KB
-    {4, 32, 32, 4, 1, 16},   // 128 px x 32, three halo slots, 148 KB
-    {8, 16, 64, 4, 1, 10},   // 128 px x 64, 16 wide (level 1: 48 columns), 128 KB
-    {6, 24, 64, 1, 4, 10},   // 144 px x 64 (level 2: 18 x 24), 136 KB
-    {9, 12, 64, 1, 4, 12},   // 108 px x 64 (level 3: the whole 9 x 12 frame), three halo slots, 156 KB
-    {9, 12, 32, 2, 2, 16},   // 108 px x 32 (level 3), three halo slots, 124 KB
-    {8, 24, 32, 2, 2, 13},   // 192 px x 32 (level 2), three halo slots, 160 KB
+    {8, 32, 64, 4, 1, 8},    // 256 px x 64: TAESD 64-channel levels, UNet level 0 (152 KB, 1 block / CU)
+    {4, 32, 64, 2, 2, 6},    // 128 px x 64 (104 KB)
+    {4, 32, 32, 4, 1, 8},    // 128 px x 32 (88 KB)
+    {8, 16, 64, 4, 1, 6},    // 128 px x 64, 16 wide (level 1: 48 columns) (96 KB)
+    {6, 24, 64, 1, 4, 6},    // 144 px x 64 (level 2: 18 x 24) (104 KB)
+    {9, 12, 64, 1, 4, 8},    // 108 px x 64 (level 3: the whole 9 x 12 frame) (104 KB)
+    {9, 12, 32, 2, 2, 8},    // 108 px x 32 (level 3) (72 KB, 2 blocks / CU)
+    {8, 24, 32, 2, 2, 4},    // 192 px x 32 (level 2) (88 KB)
     // two blocks per CU (<= 80 KB)
     {8, 16, 64, 4, 1, 4},    // 128 px x 64
     {4, 32, 64, 2, 2, 3},    // 128 px x 64
@@ -1097,6 +1129,8 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   {
     const char* e = getenv("DC_GEMM_ORDER");
     p.nmajor = (e && atoi(e) == 2) ? 1 : 0;
+    const char* dg = getenv("DC_HALO_DIAG");
+    p.diag = dg ? atoi(dg) : 0;
   }
   if (p.geglu < 0 || p.geglu > 2) return DC_ERR_ARG;
   if (p.rows && (p.nrows <= 0 || p.geglu)) return DC_ERR_ARG;

@@ -184,6 +184,18 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     return d
 
 
+HALO_FIRST = 23   # dc_conv_gemm algo ids >= this run the halo-tile direct 3x3 conv (conv_gemm.hip)
+
+
+def halo_eligible(d) -> bool:
+    """The halo kernel's contract (conv_gemm.hip halo_eligible): 3x3, stride 1, pad 1, direct or nearest-upsample
+    input, whole 64-channel chunks, no row list, no GEGLU epilogue."""
+    return (d.kh == 3 and d.kw == 3 and d.stride == 1 and d.pad == 1 and d.cin % 64 == 0 and not d.rows
+            and not d.geglu and d.mode in (0, 1) and d.ktot == 9 * d.cin
+            and (d.mode == 1 or (d.hin == d.hout and d.win == d.wout))
+            and (not d.x2 or d.c1 % 64 == 0))
+
+
 def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     """Time every (algo, splitk) variant of one conv on its own operands; returns the fastest.
 
@@ -198,8 +210,13 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     dt = ConvDesc.from_buffer_copy(d)
     dt.y = tmp.data_ptr() + (d.y - base)
     nalg = _lib.load().dc_conv_num_algos()
-    # split-K 1..32, and stream-K over 256 / 512 / 768 blocks (splitk -1 / -2 / -3)
-    cands = [(0, 0)] + [(a, s) for a in range(1, nalg + 1) for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
+    # im2col tiles: split-K 1..32, and stream-K over 256 / 512 / 768 blocks (splitk -1 / -2 / -3); halo tiles
+    # (algos > HALO_FIRST - 1, stride-1 3x3 convs over whole 64-channel chunks only): input-chunk splits
+    cands = [(0, 0)] + [(a, s) for a in range(1, min(nalg, HALO_FIRST - 1) + 1)
+                        for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
+    if halo_eligible(d):
+        cands += [(a, s) for a in range(HALO_FIRST, nalg + 1) for s in (1, 2, 3, 4, 5, 8, 10, 16, 20)
+                  if s <= d.cin // 64]
     best, best_t = (0, 0), float("inf")
     # DC_TUNE_COLD=1: every timed call starts with L2 and the Infinity Cache flushed (a 512 MiB write),
     # as the weights are in the sampler step (each is touched once per pass)

@@ -27,12 +27,21 @@ def main():
     ap.add_argument("--workloads", nargs="+", default=["c2:1", "c2:8"])
     ap.add_argument("--out", default="gpurun_out/tuned_gfx950.json")
     ap.add_argument("--fresh", action="store_true", help="ignore the committed table")
+    ap.add_argument("--retune-3x3", action="store_true",
+                    help="re-time the stride-1 3x3 shapes with cin % 64 == 0 (the halo-kernel contract) over every "
+                         "variant, keep the committed choice of every other shape")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     pipe = MarigoldDepthCompletionPipeline(synthetic.unet_state_dict(MARIGOLD_V1, 11), synthetic.taesd_state_dict(12),
                                            synthetic.text_embedding(13, 1024), device=dev, use_graph=False)
     if args.fresh:
         pipe.ctx.algo_cache = {}
+    if args.retune_3x3:
+        # key = (mode, nb, hin, win, cin, hout, wout, cout, kh, stride, two_src, ktot) (ops.conv_key)
+        keep = {k: v for k, v in pipe.ctx.algo_cache.items()
+                if not (k[8] == 3 and k[9] == 1 and k[4] % 64 == 0 and k[0] in (0, 1))}
+        print(f"re-tuning {len(pipe.ctx.algo_cache) - len(keep)} 3x3 shapes", flush=True)
+        pipe.ctx.algo_cache = keep
     pipe.ctx.tune = True
     shapes = {"c2": (576, 768, 500, "uniform"), "c3": (576, 768, 500, "uniform"), "c4": (352, 1216, 0, "beams"),
               "c5": (900, 1600, 3000, "uniform")}
