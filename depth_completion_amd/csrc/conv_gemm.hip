@@ -785,55 +785,88 @@ struct HaloBlock {
     }
   }
 
-  // one iteration (chunk c = current, tap T)
-  template <int T, bool LAST>
-  __device__ __forceinline__ void tap_step() {
-    constexpr int K = LAST ? ((S - 2) < (8 - T) ? (S - 2) : (8 - T)) : (S - 2);
-    constexpr int E = (!LAST && T + S - 2 >= 9) ? 1 : 0;
-    vm_wait<K * LW + E * LH>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // load iteration i + S - 1: chunk + (T + S - 1 >= 9), tap (T + S - 1) % 9 (none past the block's last)
-    constexpr int TT = T + S - 1;
-    if constexpr (!LAST || TT < 9) {
-      if constexpr (TT % 9 == 0) issue_halo(q_c);
-      issue_w(q_c, TT % 9);
-      if constexpr (TT % 9 == 8) ++q_c;
-    }
-    constexpr int KY = T / 3, KX = T % 3;
-    constexpr int TOFF = KY * C::HW2 + KX;
-    const char* ha = smem + cpar * C::HALO;
-    const char* wbase = smem + 2 * C::HALO + wslot * C::WST;
-    bf16x8 af[2][MI], bfr[2][NJ];
+  struct Frags {
+    bf16x8 a[2][MI], b[2][NJ];
+  };
+  // fragments of tap T from halo slot hs and weight slot ws
+  template <int T>
+  __device__ __forceinline__ void read_frags(Frags& f, int hs, int ws) {
+    constexpr int TOFF = (T / 3) * C::HW2 + T % 3;
+    const char* ha = smem + hs * C::HALO;
+    const char* wbase = smem + 2 * C::HALO + ws * C::WST;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int ii = 0; ii < MI; ++ii) {
         const int r = hbase[ii] + TOFF;
-        af[ks][ii] = *reinterpret_cast<const bf16x8*>(ha + r * RB + ((chunk ^ (r & 7)) << 4));
+        f.a[ks][ii] = *reinterpret_cast<const bf16x8*>(ha + r * RB + ((chunk ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int jj = 0; jj < NJ; ++jj) {
         const int row = wn * WN + jj * 16 + (lane & 15);
-        bfr[ks][jj] = *reinterpret_cast<const bf16x8*>(wbase + row * RB + ((chunk ^ (row & 7)) << 4));
+        f.b[ks][jj] = *reinterpret_cast<const bf16x8*>(wbase + row * RB + ((chunk ^ (row & 7)) << 4));
       }
     }
+  }
+  __device__ __forceinline__ void mfma_half(const Frags& f, int ks) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int ii = 0; ii < MI; ++ii)
 #pragma unroll
-      for (int ii = 0; ii < MI; ++ii)
-#pragma unroll
-        for (int jj = 0; jj < NJ; ++jj)
-          acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][ii], bfr[ks][jj], acc[ii][jj], 0, 0, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
+      for (int jj = 0; jj < NJ; ++jj)
+        acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[ks][ii], f.b[ks][jj], acc[ii][jj], 0, 0, 0);
+  }
+
+  // One iteration i (chunk c, tap T), fragments of i already in `cur` (software pipeline, one stage): the first
+  // k-half's MFMAs; then the wait + barrier that make iteration i + 1's slices visible, the LDS-DMA issue of
+  // iteration i + S - 1 (into the weight slot iteration i - 1 used: its fragments were read before this barrier)
+  // and the fragment reads of i + 1 into `nxt`, in the shadow of the second k-half's MFMAs.
+  // vmcnt: the loads younger than iteration i + 1's are iterations i + 2 .. i + S - 2 (issued up to i - 1), one
+  // of them carrying the next chunk's halo when tap 9 falls in [T + 2, T + S - 2]; in the last chunk only
+  // iterations up to its tap 8 follow and none carries a halo.
+  template <int T, bool LAST>
+  __device__ __forceinline__ void tap_step(Frags& cur, Frags& nxt) {
+    mfma_half(cur, 0);
+    constexpr bool HAS_NEXT = !(LAST && T == 8);
+    if constexpr (HAS_NEXT) {
+      constexpr int K = LAST ? ((S - 3) < (7 - T) ? (S - 3) : (7 - T)) : (S - 3);
+      constexpr int E = (!LAST && T + S >= 11 && T <= 7) ? 1 : 0;
+      vm_wait<(K > 0 ? K : 0) * LW + E * LH>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      constexpr int TT = T + S - 1;
+      if constexpr (!LAST || TT < 9) {
+        if constexpr (TT % 9 == 0) issue_halo(q_c);
+        issue_w(q_c, TT % 9);
+        if constexpr (TT % 9 == 8) ++q_c;
+      }
+      const int wnext = wslot + 1 == S ? 0 : wslot + 1;
+      read_frags<(T + 1) % 9>(nxt, T == 8 ? (cpar ^ 1) : cpar, wnext);
+    }
+    mfma_half(cur, 1);
+    if constexpr (HAS_NEXT) {
+      __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ, 0);          // first k-half MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);    // next fragments
+      __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ, 0);          // second k-half MFMAs
+    }
     wslot = wslot + 1 == S ? 0 : wslot + 1;
   }
-  template <bool LAST, int... T>
-  __device__ __forceinline__ void chunk_steps(std::integer_sequence<int, T...>) {
-    (tap_step<T, LAST>(), ...);
+  // the 9 taps of a chunk, fragment sets alternating f (even taps) / g (odd taps); leaves the next chunk's
+  // tap-0 fragments in f
+  template <bool LAST>
+  __device__ __forceinline__ void chunk_steps(Frags& f) {
+    Frags g;
+    tap_step<0, LAST>(f, g);
+    tap_step<1, LAST>(g, f);
+    tap_step<2, LAST>(f, g);
+    tap_step<3, LAST>(g, f);
+    tap_step<4, LAST>(f, g);
+    tap_step<5, LAST>(g, f);
+    tap_step<6, LAST>(f, g);
+    tap_step<7, LAST>(g, f);
+    tap_step<8, LAST>(f, g);
+    f = g;
   }
 
   __device__ __forceinline__ void run() {
@@ -903,25 +936,33 @@ struct HaloBlock {
     q_c = c_begin;
     q_t = 0;
     q_slot = 0;
-    const int NI = nch * 9;
-    for (int s = 0; s < S - 1 && s < NI; ++s) issue_next();
-    // after the prologue the issue cursor sits at iteration S - 1: chunk c_begin + (S-1)/9 ... (S - 1 <= 9)
     cpar = 0;
     wslot = 0;
-    for (int c = 0; c < nch; ++c) {
-      // keep the 9 taps' fragment addresses out of registers across chunks (hoisted, they cost 9 x 2 x MI VGPRs
-      // and spilled the 9-fragment variants): recomputed per tap, in the MFMAs' VALU shadow
+    if (nch > 0) {
+      // prologue: iterations 0 .. S-2 in flight (a block has >= 9 iterations, S <= 10), then iteration 0 visible
+      for (int s = 0; s < S - 1; ++s) issue_next();
+      vm_wait<(S - 2) * LW>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      Frags f;
+      read_frags<0>(f, 0, 0);
+      for (int c = 0; c < nch; ++c) {
+        // keep the 9 taps' fragment addresses out of registers across chunks (hoisted, they cost 9 x 2 x MI
+        // VGPRs and spilled the 9-fragment variants): recomputed per tap, in the MFMAs' VALU shadow
 #pragma unroll
-      for (int ii = 0; ii < MI; ++ii) asm volatile("" : "+v"(hbase[ii]));
-      if (c + 1 < nch) chunk_steps<false>(std::make_integer_sequence<int, 9>{});
-      else chunk_steps<true>(std::make_integer_sequence<int, 9>{});
-      cpar ^= 1;
+        for (int ii = 0; ii < MI; ++ii) asm volatile("" : "+v"(hbase[ii]));
+        if (c + 1 < nch) chunk_steps<false>(f);
+        else chunk_steps<true>(f);
+        cpar ^= 1;
+      }
     }
     vm_wait<0>();
 
     if (p.splits > 1 && !tile_handoff_g<MI, NJ>(p, smem, lb, split * tiles + lb, p.splits,
                                                 [&](int sp) { return sp * tiles + lb; }, acc))
       return;
+    if (p.diag & 8) return;
     epilogue();
   }
 
