@@ -738,7 +738,7 @@ struct HaloCfg {
 // of a chunk that is not the block's last, the loads younger than iteration i's are iterations i+1 .. i+S-2,
 // (S-2) LW weight pieces plus one halo when t + S - 2 >= 9; in the last chunk only min(S-2, 8-t) iterations
 // follow, none with a halo.  (A runtime-selected vmcnt was a ~450-cycle branch chain per iteration.)
-template <int TH, int TW, int BN, int WGM, int WGN, int S>
+template <int TH, int TW, int BN, int WGM, int WGN, int S, int SCHED>
 struct HaloBlock {
   using C = HaloCfg<TH, TW, BN, WGM, WGN, S>;
   static constexpr int MI = C::MI, NJ = C::NJ, WM = C::WM, WN = C::WN, RB = C::RB, LH = C::LH, LW = C::LW;
@@ -785,88 +785,67 @@ struct HaloBlock {
     }
   }
 
-  struct Frags {
-    bf16x8 a[2][MI], b[2][NJ];
-  };
-  // fragments of tap T from halo slot hs and weight slot ws
-  template <int T>
-  __device__ __forceinline__ void read_frags(Frags& f, int hs, int ws) {
-    constexpr int TOFF = (T / 3) * C::HW2 + T % 3;
-    const char* ha = smem + hs * C::HALO;
-    const char* wbase = smem + 2 * C::HALO + ws * C::WST;
+  // one iteration (chunk c = current, tap T)
+  template <int T, bool LAST>
+  __device__ __forceinline__ void tap_step() {
+    constexpr int K = LAST ? ((S - 2) < (8 - T) ? (S - 2) : (8 - T)) : (S - 2);
+    constexpr int E = (!LAST && T + S - 2 >= 9) ? 1 : 0;
+    vm_wait<K * LW + E * LH>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // load iteration i + S - 1: chunk + (T + S - 1 >= 9), tap (T + S - 1) % 9 (none past the block's last)
+    constexpr int TT = T + S - 1;
+    if constexpr (!LAST || TT < 9) {
+      if constexpr (TT % 9 == 0) issue_halo(q_c);
+      issue_w(q_c, TT % 9);
+      if constexpr (TT % 9 == 8) ++q_c;
+    }
+    constexpr int KY = T / 3, KX = T % 3;
+    constexpr int TOFF = KY * C::HW2 + KX;
+    const char* ha = smem + cpar * C::HALO;
+    const char* wbase = smem + 2 * C::HALO + wslot * C::WST;
+    bf16x8 af[2][MI], bfr[2][NJ];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int chunk = ks * 4 + (lane >> 4);
 #pragma unroll
       for (int ii = 0; ii < MI; ++ii) {
         const int r = hbase[ii] + TOFF;
-        f.a[ks][ii] = *reinterpret_cast<const bf16x8*>(ha + r * RB + ((chunk ^ (r & 7)) << 4));
+        af[ks][ii] = *reinterpret_cast<const bf16x8*>(ha + r * RB + ((chunk ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int jj = 0; jj < NJ; ++jj) {
         const int row = wn * WN + jj * 16 + (lane & 15);
-        f.b[ks][jj] = *reinterpret_cast<const bf16x8*>(wbase + row * RB + ((chunk ^ (row & 7)) << 4));
+        bfr[ks][jj] = *reinterpret_cast<const bf16x8*>(wbase + row * RB + ((chunk ^ (row & 7)) << 4));
       }
     }
-  }
-  __device__ __forceinline__ void mfma_half(const Frags& f, int ks) {
 #pragma unroll
-    for (int ii = 0; ii < MI; ++ii)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int jj = 0; jj < NJ; ++jj)
-        acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[ks][ii], f.b[ks][jj], acc[ii][jj], 0, 0, 0);
-  }
-
-  // One iteration i (chunk c, tap T), fragments of i already in `cur` (software pipeline, one stage): the first
-  // k-half's MFMAs; then the wait + barrier that make iteration i + 1's slices visible, the LDS-DMA issue of
-  // iteration i + S - 1 (into the weight slot iteration i - 1 used: its fragments were read before this barrier)
-  // and the fragment reads of i + 1 into `nxt`, in the shadow of the second k-half's MFMAs.
-  // vmcnt: the loads younger than iteration i + 1's are iterations i + 2 .. i + S - 2 (issued up to i - 1), one
-  // of them carrying the next chunk's halo when tap 9 falls in [T + 2, T + S - 2]; in the last chunk only
-  // iterations up to its tap 8 follow and none carries a halo.
-  template <int T, bool LAST>
-  __device__ __forceinline__ void tap_step(Frags& cur, Frags& nxt) {
-    mfma_half(cur, 0);
-    constexpr bool HAS_NEXT = !(LAST && T == 8);
-    if constexpr (HAS_NEXT) {
-      constexpr int K = LAST ? ((S - 3) < (7 - T) ? (S - 3) : (7 - T)) : (S - 3);
-      constexpr int E = (!LAST && T + S >= 11 && T <= 7) ? 1 : 0;
-      vm_wait<(K > 0 ? K : 0) * LW + E * LH>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      constexpr int TT = T + S - 1;
-      if constexpr (!LAST || TT < 9) {
-        if constexpr (TT % 9 == 0) issue_halo(q_c);
-        issue_w(q_c, TT % 9);
-        if constexpr (TT % 9 == 8) ++q_c;
+      for (int ii = 0; ii < MI; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj)
+          acc[ii][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks][ii], bfr[ks][jj], acc[ii][jj], 0, 0, 0);
+    if constexpr (SCHED == 0) {
+      // every fragment read of the tap ahead of its MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ, 0);
+    } else {
+      // the first k-half's reads, then its MFMAs interleaved with the second k-half's reads, then the rest
+      __builtin_amdgcn_sched_group_barrier(0x100, MI + NJ, 0);
+#pragma unroll
+      for (int q = 0; q < MI + NJ; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
-      const int wnext = wslot + 1 == S ? 0 : wslot + 1;
-      read_frags<(T + 1) % 9>(nxt, T == 8 ? (cpar ^ 1) : cpar, wnext);
-    }
-    mfma_half(cur, 1);
-    if constexpr (HAS_NEXT) {
-      __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ, 0);          // first k-half MFMAs
-      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (MI + NJ), 0);    // next fragments
-      __builtin_amdgcn_sched_group_barrier(0x008, MI * NJ, 0);          // second k-half MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * MI * NJ - (MI + NJ), 0);
     }
     wslot = wslot + 1 == S ? 0 : wslot + 1;
   }
-  // the 9 taps of a chunk, fragment sets alternating f (even taps) / g (odd taps); leaves the next chunk's
-  // tap-0 fragments in f
-  template <bool LAST>
-  __device__ __forceinline__ void chunk_steps(Frags& f) {
-    Frags g;
-    tap_step<0, LAST>(f, g);
-    tap_step<1, LAST>(g, f);
-    tap_step<2, LAST>(f, g);
-    tap_step<3, LAST>(g, f);
-    tap_step<4, LAST>(f, g);
-    tap_step<5, LAST>(g, f);
-    tap_step<6, LAST>(f, g);
-    tap_step<7, LAST>(g, f);
-    tap_step<8, LAST>(f, g);
-    f = g;
+  template <bool LAST, int... T>
+  __device__ __forceinline__ void chunk_steps(std::integer_sequence<int, T...>) {
+    (tap_step<T, LAST>(), ...);
   }
 
   __device__ __forceinline__ void run() {
@@ -936,33 +915,25 @@ struct HaloBlock {
     q_c = c_begin;
     q_t = 0;
     q_slot = 0;
+    const int NI = nch * 9;
+    for (int s = 0; s < S - 1 && s < NI; ++s) issue_next();
+    // after the prologue the issue cursor sits at iteration S - 1: chunk c_begin + (S-1)/9 ... (S - 1 <= 9)
     cpar = 0;
     wslot = 0;
-    if (nch > 0) {
-      // prologue: iterations 0 .. S-2 in flight (a block has >= 9 iterations, S <= 10), then iteration 0 visible
-      for (int s = 0; s < S - 1; ++s) issue_next();
-      vm_wait<(S - 2) * LW>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      Frags f;
-      read_frags<0>(f, 0, 0);
-      for (int c = 0; c < nch; ++c) {
-        // keep the 9 taps' fragment addresses out of registers across chunks (hoisted, they cost 9 x 2 x MI
-        // VGPRs and spilled the 9-fragment variants): recomputed per tap, in the MFMAs' VALU shadow
+    for (int c = 0; c < nch; ++c) {
+      // keep the 9 taps' fragment addresses out of registers across chunks (hoisted, they cost 9 x 2 x MI VGPRs
+      // and spilled the 9-fragment variants): recomputed per tap, in the MFMAs' VALU shadow
 #pragma unroll
-        for (int ii = 0; ii < MI; ++ii) asm volatile("" : "+v"(hbase[ii]));
-        if (c + 1 < nch) chunk_steps<false>(f);
-        else chunk_steps<true>(f);
-        cpar ^= 1;
-      }
+      for (int ii = 0; ii < MI; ++ii) asm volatile("" : "+v"(hbase[ii]));
+      if (c + 1 < nch) chunk_steps<false>(std::make_integer_sequence<int, 9>{});
+      else chunk_steps<true>(std::make_integer_sequence<int, 9>{});
+      cpar ^= 1;
     }
     vm_wait<0>();
 
     if (p.splits > 1 && !tile_handoff_g<MI, NJ>(p, smem, lb, split * tiles + lb, p.splits,
                                                 [&](int sp) { return sp * tiles + lb; }, acc))
       return;
-    if (p.diag & 8) return;
     epilogue();
   }
 
@@ -1000,29 +971,33 @@ struct HaloBlock {
   }
 };
 
-template <int TH, int TW, int BN, int WGM, int WGN, int S>
+template <int TH, int TW, int BN, int WGM, int WGN, int S, int SCHED>
 __global__ __launch_bounds__(256) void conv_halo_kernel(const ConvGemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[HaloCfg<TH, TW, BN, WGM, WGN, S>::LDS];
-  HaloBlock<TH, TW, BN, WGM, WGN, S> blk{p, smem};
+  HaloBlock<TH, TW, BN, WGM, WGN, S, SCHED> blk{p, smem};
   blk.run();
 }
 
 // halo variants: (TH, TW, BN, wave layout WGM x WGN, weight ring depth S)
 struct HaloAlgo {
-  int th, tw, bn, wgm, wgn, s;
+  int th, tw, bn, wgm, wgn, s, sched;
 };
 constexpr HaloAlgo kHaloAlgos[] = {
-    {8, 32, 64, 4, 1, 8},    // 256 px x 64: TAESD 64-channel levels, UNet level 0 (152 KB, 1 block / CU)
-    {4, 32, 64, 2, 2, 6},    // 128 px x 64 (104 KB)
-    {4, 32, 32, 4, 1, 8},    // 128 px x 32 (88 KB)
-    {8, 16, 64, 4, 1, 6},    // 128 px x 64, 16 wide (level 1: 48 columns) (96 KB)
-    {6, 24, 64, 1, 4, 6},    // 144 px x 64 (level 2: 18 x 24) (104 KB)
-    {9, 12, 64, 1, 4, 8},    // 108 px x 64 (level 3: the whole 9 x 12 frame) (104 KB)
-    {9, 12, 32, 2, 2, 8},    // 108 px x 32 (level 3) (72 KB, 2 blocks / CU)
-    {8, 24, 32, 2, 2, 4},    // 192 px x 32 (level 2) (88 KB)
-    // two blocks per CU (<= 80 KB)
-    {8, 16, 64, 4, 1, 4},    // 128 px x 64
-    {4, 32, 64, 2, 2, 3},    // 128 px x 64
+    // (sched 0: a tap's fragment reads all ahead of its MFMAs; 1: second k-half's reads under the first's MFMAs)
+    {8, 32, 64, 4, 1, 8, 0},    // 256 px x 64: TAESD 64-channel levels, UNet level 0 (152 KB, 1 block / CU)
+    {4, 32, 64, 2, 2, 6, 0},    // 128 px x 64 (104 KB)
+    {4, 32, 32, 4, 1, 8, 0},    // 128 px x 32 (88 KB)
+    {8, 16, 64, 4, 1, 6, 0},    // 128 px x 64, 16 wide (level 1: 48 columns) (96 KB)
+    {6, 24, 64, 1, 4, 6, 0},    // 144 px x 64 (level 2: 18 x 24) (104 KB)
+    {9, 12, 64, 1, 4, 8, 0},    // 108 px x 64 (level 3: the whole 9 x 12 frame) (104 KB)
+    {9, 12, 32, 2, 2, 8, 0},    // 108 px x 32 (level 3) (72 KB, 2 blocks / CU)
+    {8, 24, 32, 2, 2, 4, 0},    // 192 px x 32 (level 2) (88 KB)
+    {8, 16, 64, 4, 1, 4, 0},    // 128 px x 64 (80 KB, 2 blocks / CU)
+    {4, 32, 64, 2, 2, 3, 0},    // 128 px x 64 (80 KB, 2 blocks / CU)
+    {8, 16, 64, 4, 1, 4, 1},    // the two-blocks-per-CU forms, interleaved schedule
+    {4, 32, 64, 2, 2, 3, 1},
+    {8, 32, 64, 4, 1, 8, 1},
+    {6, 24, 64, 1, 4, 6, 1},
 };
 
 constexpr long kCounterBytes = 64 * 1024;
@@ -1043,9 +1018,9 @@ constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 
 constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
 constexpr int kNumHalo = sizeof(kHaloAlgos) / sizeof(kHaloAlgos[0]);
 constexpr int kNumAll = kNumAlgos + kNumHalo;   // algo ids kNumAlgos + 1 .. kNumAll: halo variants
-static_assert(kNumHalo == 10, "DC_HALO cases below");
+static_assert(kNumHalo == 14, "DC_HALO cases below");
 
-template <int TH, int TW, int BN, int WGM, int WGN, int S>
+template <int TH, int TW, int BN, int WGM, int WGN, int S, int SCHED>
 int launch_halo(ConvGemmParams& p, int splits, hipStream_t stream) {
   using Cf = HaloCfg<TH, TW, BN, WGM, WGN, S>;
   const long tiles_l = (long)p.nb * ((p.hout + TH - 1) / TH) * ((p.wout + TW - 1) / TW) * ((p.cout + BN - 1) / BN);
@@ -1060,7 +1035,7 @@ int launch_halo(ConvGemmParams& p, int splits, hipStream_t stream) {
   splits = (nck + p.kps - 1) / p.kps;
   p.splits = splits;
   p.sk_blocks = 0;
-  hipLaunchKernelGGL((conv_halo_kernel<TH, TW, BN, WGM, WGN, S>), dim3(tiles, splits), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((conv_halo_kernel<TH, TW, BN, WGM, WGN, S, SCHED>), dim3(tiles, splits), dim3(256), 0, stream, p);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -1212,9 +1187,9 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
 #define DC_HALO(i)                                                                                              \
   case i:                                                                                                       \
     return launch_halo<kHaloAlgos[i].th, kHaloAlgos[i].tw, kHaloAlgos[i].bn, kHaloAlgos[i].wgm, kHaloAlgos[i].wgn, \
-                       kHaloAlgos[i].s>(p, splits == 0 ? 1 : splits, s);
+                       kHaloAlgos[i].s, kHaloAlgos[i].sched>(p, splits == 0 ? 1 : splits, s);
         DC_HALO(0) DC_HALO(1) DC_HALO(2) DC_HALO(3) DC_HALO(4) DC_HALO(5) DC_HALO(6) DC_HALO(7) DC_HALO(8)
-        DC_HALO(9)
+        DC_HALO(9) DC_HALO(10) DC_HALO(11) DC_HALO(12) DC_HALO(13)
 #undef DC_HALO
         default: return DC_ERR_ARG;
       }

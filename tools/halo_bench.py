@@ -79,6 +79,7 @@ def main():
         ref = y0.clone()
         flops = 2.0 * nb * hout * wout * cout * 9 * cin
         best = (float("inf"), None, 0.0)
+        per_algo = {}
         for a in halo:
             for sp in (1, 2, 3, 4, 5, 8, 10, 16):
                 if sp > cin // 64:
@@ -91,9 +92,13 @@ def main():
                     print(f"   !! algo {a} split {sp}: rel err {err:.3e}", flush=True)
                 if t < best[0]:
                     best = (t, (a, sp), err)
+                if t < per_algo.get(a, (float("inf"),))[0]:
+                    per_algo[a] = (t, sp)
         print(f"nb={nb} {hin}x{win}->{hout}x{wout} cin={cin} cout={cout} mode={mode}: tuned {tuned} {t0:7.1f} us "
               f"({flops / t0 / 1e6:6.0f} TF/s) | best halo {best[1]} {best[0]:7.1f} us ({flops / best[0] / 1e6:6.0f} "
               f"TF/s, err {best[2]:.1e}) x{t0 / best[0]:.2f}", flush=True)
+        top = sorted(per_algo.items(), key=lambda kv: kv[1][0])
+        print("      " + "  ".join(f"{a}/{sp}:{t:.1f}" for a, (t, sp) in top), flush=True)
 
 
 if __name__ == "__main__":
