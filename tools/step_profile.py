@@ -1,0 +1,117 @@
+"""Per-shape conv time inside the real graph-replayed guided step (GPU, run under rocprofv3 --kernel-trace).
+
+Run:   rocprofv3 --kernel-trace -d <dir> -o run --output-format csv -- python3 tools/step_profile.py --out <descs.json>
+       python tools/step_profile.py --trace <dir>/run_kernel_trace.csv --descs <descs.json>
+The first form runs a C2 call (graph-replayed guided steps) and writes the conv launches of one step, in launch
+order, with their shapes and chosen variants.  The second (CPU) takes the last complete step of the trace, matches
+its conv dispatches (conv_gemm_kernel / conv_halo_kernel) to those launches by order, and prints the time per shape
+group -- the step's own cache state and launch order, unlike tools/conv_breakdown.py's warm replays.
+"""
+import argparse
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def record(out, batch):
+    import torch
+    from bench import conv_flops, synth_frame
+    from depth_completion_amd import ops, synthetic
+    from depth_completion_amd._lib import ConvDesc
+    from depth_completion_amd.config import MARIGOLD_V1
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    dev = torch.device("cuda:0")
+    pipe = MarigoldDepthCompletionPipeline(synthetic.unet_state_dict(MARIGOLD_V1, 11), synthetic.taesd_state_dict(12),
+                                           synthetic.text_embedding(13, 1024), device=dev)
+    fr = [synth_frame(576, 768, 500, i) for i in range(batch)]
+    imgs = torch.stack([f[0] for f in fr]).to(dev)
+    sps = torch.stack([f[1] for f in fr]).to(dev)
+    for _ in range(2):
+        pipe(imgs, sps, 120.0, norm="const", steps=8, resolution=768)
+    torch.cuda.synchronize()
+    st = pipe._plans[(batch, 72, 96)]
+    descs = []
+    orig = ops.call
+
+    def rec(name, *a):
+        if name == "dc_conv_gemm":
+            d = ConvDesc.from_buffer_copy(a[0]._obj)
+            descs.append(dict(M=d.nb * d.hout * d.wout, rows=int(d.nrows) if d.rows else 0, N=d.cout,
+                              K=d.kh * d.kw * d.cin, cin=d.cin, mode=d.mode, k=d.kh, stride=d.stride,
+                              hw=[d.hout, d.wout], algo=int(d.algo), split=int(d.splitk), flops=conv_flops(d)))
+        return orig(name, *a)
+
+    # the captured step's launch sequence: record while capturing a throwaway graph (nothing runs)
+    st["dec"].set_rows(st.get("row_sets"))
+    g = torch.cuda.CUDAGraph()
+    ops.call = rec
+    try:
+        with torch.cuda.graph(g):
+            pipe._step(st)
+    finally:
+        ops.call = orig
+        st["dec"].set_rows(None)
+    with open(out, "w") as f:
+        json.dump(descs, f)
+    print(f"{len(descs)} conv launches per step recorded", flush=True)
+
+
+def analyse(trace, descs_path):
+    descs = json.load(open(descs_path))
+    rows = []
+    with open(trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    conv = [r for r in rows if "conv_gemm_kernel" in r[2] or "conv_halo_kernel" in r[2]]
+    n = len(descs)
+    last = conv[-n:]   # the final step of the last call is the last n conv dispatches (final decode is dense:
+    # skip back over the final decode's convs by aligning on shapes below)
+    # align: the final decode after the loop adds TAESD convs; find the window whose count matches the step
+    best = None
+    for off in range(0, min(len(conv) - n, 200) + 1):
+        win = conv[len(conv) - n - off:len(conv) - off]
+        ok = sum(("halo" in w[2]) == (d["algo"] >= 23) for w, d in zip(win, descs))
+        if best is None or ok > best[0]:
+            best = (ok, win)
+        if ok == n:
+            break
+    ok, win = best
+    print(f"aligned {ok}/{n} launches by kernel family")
+    groups = defaultdict(lambda: [0, 0.0, 0.0, set()])
+    tot = 0.0
+    for (s, e, name), d in zip(win, descs):
+        us = (e - s) / 1e3
+        key = (d["M"], d["N"], d["K"], d["mode"], d["k"], d["stride"], d["rows"] > 0)
+        g = groups[key]
+        g[0] += 1
+        g[1] += us
+        g[2] += d["flops"]
+        g[3].add((d["algo"], d["split"]))
+        tot += us
+    print(f"conv time in one step: {tot / 1e3:.3f} ms over {n} launches")
+    for key, (cnt, us, fl, algos) in sorted(groups.items(), key=lambda kv: -kv[1][1]):
+        M, N, K, mode, k, stride, rl = key
+        print(f"M={M:7d}{'r' if rl else ' '} N={N:5d} K={K:6d} mode={mode} k={k} s={stride} x{cnt:3d}: {us:8.1f} us "
+              f"({100 * us / tot:5.1f} %) {fl / (us * 1e-6) / 1e12:7.1f} TF/s  {sorted(algos)}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out")
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--trace")
+    ap.add_argument("--descs")
+    a = ap.parse_args()
+    if a.trace:
+        analyse(a.trace, a.descs)
+    else:
+        record(a.out, a.batch)
+
+
+if __name__ == "__main__":
+    main()
