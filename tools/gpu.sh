@@ -14,6 +14,7 @@
 #   trace3                     the same for C3 (batch 8)
 #   pmc                        FETCH_SIZE and WRITE_SIZE passes over the conv kernel (eager C2, 4 denoise steps)
 #   breakdown[=<batch>]        per-shape conv breakdown of one guided step (tools/conv_breakdown.py)
+#   stepprof                   per-shape conv time inside the graph-replayed step (tools/step_profile.py)
 #   py=<script args>           any repo python script (e.g. py=tools/gemm_one.py --m 6912)
 set -e
 tag=${1:?tag}
@@ -62,6 +63,11 @@ for step in "$@"; do
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex conv_gemm -d "$out/pmc_write" -o run \
         --output-format csv -- python3 bench.py --no-graph --steps 1 --warmup 0 --no-cpu-baseline --denoise-steps 4 \
         > "$out/pmc_write.json" 2> "$out/pmc_write.err" ;;
+    stepprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$out/steptrace" -o run --output-format csv -- \
+        python3 tools/step_profile.py --out "$out/descs.json" > "$out/stepprof.log" 2>&1
+      python3 tools/step_profile.py --trace "$out/steptrace/run_kernel_trace.csv" --descs "$out/descs.json" \
+        > "$out/step_shapes.txt" 2>&1 ;;
     breakdown)
       timeout -k 10 300 python -u tools/conv_breakdown.py > "$out/conv_breakdown.txt" 2> "$out/conv_breakdown.err" ;;
     breakdown=*)
