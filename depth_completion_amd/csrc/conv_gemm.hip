@@ -179,6 +179,22 @@ __device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, 
   }
 }
 
+// -DDC_DEBUG_LDS (debug builds only, tools/debug_lds.sh): every LDS-DMA wave-instruction's 1 KiB destination and
+// every epilogue staging row is asserted inside the block's static LDS allocation
+#ifdef DC_DEBUG_LDS
+#define DC_LDS_ASSERT(off, bytes, limit)                                                                  \
+  do {                                                                                                    \
+    const int dc_o_ = (off);                                                                              \
+    if (dc_o_ < 0 || dc_o_ + (bytes) > (limit)) {                                                         \
+      printf("DC_DEBUG_LDS %s:%d block %d thread %d: LDS offset %d + %d outside %d\n", __FILE__, __LINE__, \
+             (int)blockIdx.x, (int)threadIdx.x, dc_o_, (int)(bytes), (int)(limit));                       \
+      __builtin_trap();                                                                                   \
+    }                                                                                                     \
+  } while (0)
+#else
+#define DC_LDS_ASSERT(off, bytes, limit) ((void)0)
+#endif
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -372,6 +388,12 @@ __device__ __forceinline__ void tile_pass(const ConvGemmParams& p, char* smem, l
 
   auto issue = [&](int stage) __attribute__((always_inline)) {
     DC_LDS char* sbase = (DC_LDS char*)smem + stage * STAGE;
+#ifdef DC_DEBUG_LDS
+    for (int j = 0; j < AP; ++j)
+      DC_LDS_ASSERT(stage * STAGE + (wid_s * 64 + 256 * j) * 16, 1024, (Cfg<BM, BN, BK, S>::LDS));
+    for (int j = 0; j < BP; ++j)
+      DC_LDS_ASSERT(stage * STAGE + BM * RB + (wid_s * 64 + 256 * j) * 16, 1024, (Cfg<BM, BN, BK, S>::LDS));
+#endif
     if (!SMALLC) {
       if (q_c >= p.c1) {  // uniform: the chunk comes from the second concat source
 #pragma unroll
@@ -538,6 +560,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
   __syncthreads();  // every wave is done reading the ring
   constexpr int LDE = WN + 8;
   bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
+  DC_LDS_ASSERT((wid * WM * LDE) * 2, WM * LDE * 2, (Cfg<BM, BN, 64, 2>::EPI));
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = n0 + wn * WN + j * 16 + col_l;
@@ -1161,7 +1184,11 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
+#ifdef DC_EXPERIMENT_S5
+  if (d->algo < 0 || d->algo > kNumAll + 1 || d->splitk < -4) return DC_ERR_ARG;
+#else
   if (d->algo < 0 || d->algo > kNumAll || d->splitk < -4) return DC_ERR_ARG;
+#endif
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;
@@ -1181,6 +1208,10 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   const long M = p.rows ? p.nrows : (long)p.nb * p.hout * p.wout;
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
+#ifdef DC_EXPERIMENT_S5
+  // round-2's aborted 5-stage 64x64 ring (profiles/r02zc), for tools/debug_lds.sh only
+  if (algo == kNumAll + 1) return launch_algo<64, 64, 64, 5>(p, M, splits == 0 ? 1 : splits, smallc, s);
+#endif
   if (algo > kNumAlgos) {
     if (halo_eligible(p)) {
       switch (algo - kNumAlgos - 1) {
