@@ -11,13 +11,29 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 vp = C.c_void_p
 i32 = C.c_int
 i64 = C.c_longlong
 f32 = C.c_float
 fp = C.POINTER(C.c_float)
+
+
+class GnTarget(C.Structure):
+    """Mirror of ``dc_gn_target`` (include/dcamd.h)."""
+
+    _fields_ = [("acc", vp), ("coff", i32), ("groups", i32), ("cpg", i32), ("hw", i32)]
+
+
+class GnFuse(C.Structure):
+    """Mirror of ``dc_gn_fuse``: GroupNorm statistics fused into a conv epilogue."""
+
+    _fields_ = [
+        ("mode", i32), ("nt", i32), ("t", GnTarget * 2),
+        ("x", vp), ("x2", vp), ("ldx", i32), ("ldx2", i32), ("c1", i32),
+        ("stats", vp), ("gamma", vp), ("beta", vp), ("silu", i32),
+    ]
 
 
 class ConvDesc(C.Structure):
@@ -34,7 +50,7 @@ class ConvDesc(C.Structure):
         ("y", vp), ("ldy", i32),
         ("ws", vp), ("ws_bytes", i64),
         ("geglu", i32), ("y2", vp), ("ldy2", i32), ("aux", vp), ("ldaux", i32),
-        ("algo", i32), ("splitk", i32), ("rows", vp), ("nrows", i32),
+        ("algo", i32), ("splitk", i32), ("rows", vp), ("nrows", i32), ("gn", C.POINTER(GnFuse)),
     ]
 
 
@@ -48,6 +64,11 @@ _SIGS = {
     "dc_groupnorm_fwd": [vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, i32, vp, vp, vp],
     "dc_groupnorm_bwd": [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp, i32,
                          vp, i32, vp, vp],
+    "dc_gn_acc_bytes": [i32, i32],
+    "dc_gn_fuse_pays": [i32, i32, i32, i32],
+    "dc_groupnorm_fwd_acc": [vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp, vp],
+    "dc_groupnorm_bwd_acc": [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp, i32,
+                             vp, i32, vp],
     "dc_layernorm_fwd": [vp, i32, i64, i32, f32, vp, vp, vp, i32, vp, vp],
     "dc_layernorm_bwd": [vp, i32, i64, i32, vp, vp, vp, i32, vp, i32, vp, i32, vp],
     "dc_attn_fwd": [vp, i32, i32, i32, i32, vp, i32, vp, vp, i64, vp],
@@ -117,7 +138,7 @@ _SIGS.update({
     "dc_complete": [vp, vp, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp],
 })
 _RESTYPE = {"dc_session_error": C.c_char_p, "dc_sample_params_default": None,
-            "dc_build_id": C.c_char_p, "dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64,
+            "dc_build_id": C.c_char_p, "dc_mask_rows_ws_bytes": i64, "dc_groupnorm_ws_bytes": i64, "dc_gn_acc_bytes": i64, "dc_dense_loss_ws_bytes": i64, "dc_depth_metrics_ws_bytes": i64,
              "dc_ensemble_ws_bytes": i64, "dc_crossattn_tables_bytes": i64}
 
 STATUS = {0: "ok", 1: "invalid argument / shape", 2: "kernel launch failed", 3: "alignment contract violated"}

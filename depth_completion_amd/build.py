@@ -16,16 +16,18 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libdcamd.so"
 OBJ_DIR = PKG / "build_obj"
-SOURCES = ["conv_gemm.hip", "norms.hip", "attention.hip", "crossattn.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
+SOURCES = ["conv_gemm.hip", "conv_gemm_gn.hip", "conv_gemm_gnb.hip", "norms.hip", "attention.hip", "crossattn.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
            "rowsets.hip", "ensemble.hip", "host_tables.cpp", "session.cpp", "version.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DC_OFFLOAD_ARCH", "gfx950")
+HEADERS = [CSRC / h for h in ("common.h", "gn_acc.h", "conv_gemm_impl.h", "json_mini.h", "safetensors_mini.h")] + \
+    [PKG.parent / "include" / "dcamd.h"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
 
 def source_files() -> list[Path]:
     """Every file libdcamd.so is compiled from (the build id hashes exactly these)."""
-    return [CSRC / s for s in SOURCES] + [CSRC / "common.h", CSRC / "json_mini.h", CSRC / "safetensors_mini.h", PKG.parent / "include" / "dcamd.h"]
+    return [CSRC / s for s in SOURCES] + HEADERS
 
 
 def source_hash() -> str:
@@ -46,7 +48,7 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
 
 def build(verbose: bool = False, force: bool = False) -> Path:
     OBJ_DIR.mkdir(exist_ok=True)
-    headers = [CSRC / "common.h", CSRC / "json_mini.h", CSRC / "safetensors_mini.h", PKG.parent / "include" / "dcamd.h"]
+    headers = HEADERS
     bid = source_hash()
     jobs = []
     for src in SOURCES:

@@ -12,6 +12,7 @@
 // see gn_group_fwd_kernel.
 // The input may be two sources (UNet skip concat): channels >= c1 come from x2.
 #include "common.h"
+#include "gn_acc.h"
 #include "../../include/dcamd.h"
 
 #include <initializer_list>
@@ -139,6 +140,18 @@ __device__ void gn_fold_in_block(const GNShape& s, const float* part_n, int mode
   __syncthreads();
 }
 
+// One-pass form (dc_groupnorm_*_acc): the frame's 2 G quantities accumulated by the producing convs' epilogues
+// (gn_acc.h, exact sums over the replicas) -> grp[G][2] in LDS, as gn_fold_in_block leaves it.  red: 2 G doubles.
+__device__ void gn_acc_groups(const GNShape& s, const unsigned long long* acc_n, int mode, float eps, double* red,
+                              float* grp) {
+  const int tid = threadIdx.x;
+  const long rstride = (long)s.nb * s.groups * kGnPair;
+  if (tid < 2 * s.groups) red[tid] = gn_acc_read(acc_n + (long)(tid >> 1) * kGnPair + (tid & 1) * kGnWords, rstride);
+  __syncthreads();
+  if (tid < s.groups) gn_final_pair(red[2 * tid], red[2 * tid + 1], (double)s.hw * s.cpg, eps, mode, grp + tid * 2);
+  __syncthreads();
+}
+
 __global__ void gn_stats_kernel(GNShape s, float* part) {
   extern __shared__ float sh[];
   const int n = blockIdx.y, chunk = blockIdx.x;
@@ -202,18 +215,24 @@ __global__ void gn_finalize_kernel(GNShape s, const float* part, float eps, int 
 // are computed once per thread and the row loop carries no divisions.
 // part != nullptr: the block first folds the frame's chunk partials itself (gn_fold_in_block) and block 0 of
 // the frame stores (mean, rstd) to stats for the backward; otherwise stats comes from gn_finalize_kernel.
+// acc != nullptr: the one-pass form, (mean, rstd) from the fused accumulators (gn_acc_groups)
 __global__ void gn_apply_kernel(GNShape s, const float* part, float eps, float* stats, const float* gamma,
-                                const float* beta, int silu, bf16* y, int ldy) {
+                                const float* beta, int silu, bf16* y, int ldy, const unsigned long long* acc) {
   extern __shared__ double gsh[];
   const int n = blockIdx.y;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
   const float* st = stats + (long)n * s.groups * 2;
   const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows), row0 = rbeg + r0;
   // the first row's loads go out with the fold's partial loads: one memory round trip before the first barrier
-  const bool pf = s.pf && part && r0 < s.R && row0 < rend;
+  const bool pf = s.pf && (part || acc) && r0 < s.R && row0 < rend;
   float f0[8];
   if (pf) gn_load8(s, n, row0, cg * 8, f0);
-  if (part) {
+  if (acc) {
+    float* grp = reinterpret_cast<float*>(gsh + 2 * s.groups);
+    gn_acc_groups(s, acc + (long)n * s.groups * kGnPair, 0, eps, gsh, grp);
+    if (blockIdx.x == 0 && threadIdx.x < s.groups * 2) stats[(long)n * s.groups * 2 + threadIdx.x] = grp[threadIdx.x];
+    st = grp;
+  } else if (part) {
     float* grp = reinterpret_cast<float*>(gsh + blockDim.x * 4);
     gn_fold_in_block(s, part + (long)n * s.nchunk * s.groups * 2, 0, eps, gsh, grp);
     if (blockIdx.x == 0 && threadIdx.x < s.groups * 2) stats[(long)n * s.groups * 2 + threadIdx.x] = grp[threadIdx.x];
@@ -294,21 +313,27 @@ __global__ void gn_bwd_stats_kernel(GNShape s, const float* stats, const float* 
 
 // part != nullptr: (ma, mb) folded by the block itself from the frame's chunk partials (gn_fold_in_block),
 // otherwise read from ab (gn_finalize_kernel)
+// acc != nullptr: the one-pass form (dy = the producer's stored dy', silu 0), (ma, mb) from the fused accumulators
 __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* gamma, const float* beta, int silu,
                                     const bf16* dy, int lddy, const float* part, const float* ab, bf16* dx, int lddx,
-                                    const bf16* add1, int ldadd1, const bf16* add2, int ldadd2) {
+                                    const bf16* add1, int ldadd1, const bf16* add2, int ldadd2,
+                                    const unsigned long long* acc) {
   extern __shared__ double gsh[];
   const int n = blockIdx.y;
   const int cg = threadIdx.x % s.cgs, r0 = threadIdx.x / s.cgs;
   const float* abn = ab + (long)n * s.groups * 2;
   const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows), row0 = rbeg + r0;
-  const bool pf = s.pf && part && r0 < s.R && row0 < rend;  // as gn_apply_kernel
+  const bool pf = s.pf && (part || acc) && r0 < s.R && row0 < rend;  // as gn_apply_kernel
   float f0[8], d0[8];
   if (pf) {
     gn_load8(s, n, row0, cg * 8, f0);
     load8(dy + ((long)n * s.hw + row0) * lddy + cg * 8, d0);
   }
-  if (part) {
+  if (acc) {
+    float* grp = reinterpret_cast<float*>(gsh + 2 * s.groups);
+    gn_acc_groups(s, acc + (long)n * s.groups * kGnPair, 1, 0.0f, gsh, grp);
+    abn = grp;
+  } else if (part) {
     float* grp = reinterpret_cast<float*>(gsh + blockDim.x * 4);
     gn_fold_in_block(s, part + (long)n * s.nchunk * s.groups * 2, 1, 0.0f, gsh, grp);
     abn = grp;
@@ -705,7 +730,7 @@ extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2
     hipLaunchKernelGGL(gn_finalize_kernel, dim3((groups + 3) / 4, nb), dim3(256), 0, st, s, ws, eps, 0, stats);
   const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
   hipLaunchKernelGGL(gn_apply_kernel, agrid, dim3(threads), flds, st, s, flds ? ws : nullptr, eps, stats, gamma,
-                     beta, silu, (bf16*)y, ldy);
+                     beta, silu, (bf16*)y, ldy, (const unsigned long long*)nullptr);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
@@ -745,7 +770,61 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
   hipLaunchKernelGGL(gn_bwd_apply_kernel, agrid, dim3(threads), flds, st, s, stats, gamma, beta, silu,
                      (const bf16*)dy, lddy, flds ? ws : nullptr, ab, (bf16*)dx, lddx, (const bf16*)add1, ldadd1,
-                     (const bf16*)add2, ldadd2);
+                     (const bf16*)add2, ldadd2, (const unsigned long long*)nullptr);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+// whether the fused statistics pay for this GroupNorm: not where the single-launch form (one block per (frame, group),
+// the slice stashed in LDS) runs it -- its one launch costs about what the fused producer epilogue adds
+// (tools/gn_fuse_bench.py)
+extern "C" int dc_gn_fuse_pays(int hw, int c, int groups, int backward) {
+  if (hw <= 0 || c <= 0 || groups <= 0 || c % groups) return 0;
+  GNShape s;
+  alignas(16) static const bf16 dummy[8] = {};
+  if (!gn_make_shape(s, dummy, c, nullptr, 0, 0, 1, hw, c, groups)) return 0;
+  return gn_group_vec(s, backward ? 2 : 1, backward ? kGroupCapBwd : kGroupCapFwd, {dummy}) ? 0 : 1;
+}
+
+extern "C" long long dc_gn_acc_bytes(int nb, int groups) {
+  if (nb <= 0 || groups <= 0) return -1;
+  return (long long)kGnReplicas * nb * groups * kGnPair * 8;
+}
+
+// one-pass GroupNorm from the fused statistics: the elementwise pass with the accumulator read at its head
+extern "C" int dc_groupnorm_fwd_acc(const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c,
+                                    int groups, float eps, const float* gamma, const float* beta, int silu,
+                                    const long long* acc, void* y, int ldy, float* stats, void* stream) {
+  GNShape s;
+  if (!gn_make_shape(s, x, ldx, x2, ldx2, c1, nb, hw, c, groups) || !y || !gamma || !beta || !acc || !stats)
+    return DC_ERR_ARG;
+  if (ldy % 8 || ((uintptr_t)acc & 7)) return DC_ERR_ALIGN;
+  const int threads = s.cgs * s.R;
+  if (threads < 2 * groups) return DC_ERR_ARG;
+  const size_t lds = (size_t)groups * 2 * (sizeof(double) + sizeof(float));
+  const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
+  hipLaunchKernelGGL(gn_apply_kernel, agrid, dim3(threads), lds, (hipStream_t)stream, s, (const float*)nullptr, eps,
+                     stats, gamma, beta, silu, (bf16*)y, ldy, (const unsigned long long*)acc);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+extern "C" int dc_groupnorm_bwd_acc(const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c,
+                                    int groups, const float* gamma, const float* stats, const long long* acc,
+                                    const void* dyp, int lddy, void* dx, int lddx, const void* add1, int ldadd1,
+                                    const void* add2, int ldadd2, void* stream) {
+  GNShape s;
+  if (!gn_make_shape(s, x, ldx, x2, ldx2, c1, nb, hw, c, groups) || !dyp || !dx || !stats || !gamma || !acc)
+    return DC_ERR_ARG;
+  if (lddy % 8 || lddx % 8 || (add1 && ldadd1 % 8) || (add2 && ldadd2 % 8) || ((uintptr_t)acc & 7))
+    return DC_ERR_ALIGN;
+  const int threads = s.cgs * s.R;
+  if (threads < 2 * groups) return DC_ERR_ARG;
+  const size_t lds = (size_t)groups * 2 * (sizeof(double) + sizeof(float));
+  const dim3 agrid((hw + s.apply_rows - 1) / s.apply_rows, nb);
+  hipLaunchKernelGGL(gn_bwd_apply_kernel, agrid, dim3(threads), lds, (hipStream_t)stream, s, stats, gamma, gamma, 0,
+                     (const bf16*)dyp, lddy, (const float*)nullptr, stats, (bf16*)dx, lddx, (const bf16*)add1, ldadd1,
+                     (const bf16*)add2, ldadd2, (const unsigned long long*)acc);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

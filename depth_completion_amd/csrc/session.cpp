@@ -287,6 +287,7 @@ struct Exec {
     RB y2, aux;
     const int* rows = nullptr;
     int nrows = 0;
+    const dc_gn_fuse* gn = nullptr;   // fused GroupNorm statistics (unet.py _gnf / _gn_bwd_fuse)
   };
   void conv(const Conv& a) {
     dc_conv_desc d;
@@ -319,6 +320,7 @@ struct Exec {
     d.ldaux = a.aux.p ? a.aux.ld : 0;
     d.ws = ws;
     d.ws_bytes = ws_bytes;
+    d.gn = a.gn;
     if (a.rows) {
       d.rows = a.rows;
       d.nrows = a.nrows;
@@ -345,7 +347,8 @@ struct Exec {
   }
   // ops.linear
   void linear(RB x, const void* w, int k, int rows, int cout, RB y, const float* bias = nullptr, RB resid = RB(),
-              const void* rowbias = nullptr, int rowbias_ld = 0, int geglu = 0, RB y2 = RB(), RB aux = RB()) {
+              const void* rowbias = nullptr, int rowbias_ld = 0, int geglu = 0, RB y2 = RB(), RB aux = RB(),
+              const dc_gn_fuse* gn = nullptr) {
     Conv a;
     a.x = x;
     a.nb = 1; a.hin = 1; a.win = rows; a.cin = k; a.hout = 1; a.wout = rows; a.cout = cout;
@@ -360,6 +363,7 @@ struct Exec {
     a.geglu = geglu;
     a.y2 = y2;
     a.aux = aux;
+    a.gn = gn;
     conv(a);
   }
   void groupnorm(RB x, int nb, int hw, int c, const NormW& n, bool silu, RB y, float* stats, RB x2 = RB(),
@@ -372,6 +376,17 @@ struct Exec {
     DCK(dc_groupnorm_bwd(x.p, x.ld, x2.p, x2.p ? x2.ld : 0, c1, nb, hw, c, 32, n.gamma, n.beta, silu ? 1 : 0, stats,
                          dy.p, dy.ld, dx.p, dx.ld, add1.p, add1.p ? add1.ld : 0, add2.p, add2.p ? add2.ld : 0, ws,
                          stream));
+  }
+  // ops.groupnorm_acc / ops.groupnorm_bwd_acc (fused statistics)
+  void groupnorm_acc(RB x, int nb, int hw, int c, const NormW& n, bool silu, const long long* acc, RB y, float* stats,
+                     RB x2 = RB(), int c1 = 0) {
+    DCK(dc_groupnorm_fwd_acc(x.p, x.ld, x2.p, x2.p ? x2.ld : 0, c1, nb, hw, c, 32, n.eps, n.gamma, n.beta,
+                             silu ? 1 : 0, acc, y.p, y.ld, stats, stream));
+  }
+  void groupnorm_bwd_acc(RB x, int nb, int hw, int c, const NormW& n, const float* stats, const long long* acc, RB dy,
+                         RB dx, RB x2 = RB(), int c1 = 0, RB add1 = RB(), RB add2 = RB()) {
+    DCK(dc_groupnorm_bwd_acc(x.p, x.ld, x2.p, x2.p ? x2.ld : 0, c1, nb, hw, c, 32, n.gamma, stats, acc, dy.p, dy.ld,
+                             dx.p, dx.ld, add1.p, add1.p ? add1.ld : 0, add2.p, add2.p ? add2.ld : 0, stream));
   }
   void memset0(void* p, size_t bytes) { DCK(dc_memset_async(p, 0, (long long)bytes, stream)); }
 };
@@ -578,6 +593,18 @@ class UNetPlan {
     v = buf(P, 8);
     dv = buf(P, 8);
     gx = buf(P, 8);
+    // fused GroupNorm statistics (unet.py UNetPlan.fuse_gn): one accumulator per GroupNorm and direction in one
+    // arena, zero-filled at the head of every forward
+    const char* e = getenv("DC_GN_FUSE");
+    fuse_gn_ = !(e && std::string(e) == "0");
+    int n_res = 0, n_tr = 1;
+    for (auto& b : net.down) { n_res += (int)b.res.size(); n_tr += (int)b.att.size(); }
+    for (auto& b : net.up) { n_res += (int)b.res.size(); n_tr += (int)b.att.size(); }
+    n_res += (int)net.mid_res.size();
+    const int n_gn = 2 * (2 * n_res + n_tr + 1);
+    gn_words_ = (size_t)dc_gn_acc_bytes(nb, 32) / 8;
+    gn_arena_bytes_ = (size_t)n_gn * gn_words_ * 8;
+    gn_arena_ = (long long*)mem_.alloc(gn_arena_bytes_);
     build_forward();
     build_backward();
   }
@@ -601,6 +628,70 @@ class UNetPlan {
     ConvW* cv = nullptr;
   };
   std::vector<TapeEntry> tape_;
+  bool fuse_gn_ = true;
+  long long* gn_arena_ = nullptr;
+  size_t gn_words_ = 0, gn_arena_bytes_ = 0;
+  int gn_next_ = 0;
+  std::map<const void*, std::vector<dc_gn_target>> gn_targets_;       // output buffer -> GroupNorms it feeds
+  std::map<const void*, std::unique_ptr<dc_gn_fuse>> gn_fuse_;        // built at the first call
+  std::vector<std::unique_ptr<dc_gn_fuse>> gn_bwd_;                     // backward fuses (fixed at build)
+
+  long long* gn_acc() { return gn_arena_ + (size_t)(gn_next_++) * gn_words_; }
+  bool gn_pays(int hw, int c, bool backward) { return fuse_gn_ && dc_gn_fuse_pays(hw, c, 32, backward ? 1 : 0); }
+  long long* gn_consumer(RB x, int c, int hw, RB x2 = RB(), int c1 = 0) {
+    if (!gn_pays(hw, c, false)) return nullptr;
+    long long* acc = gn_acc();
+    const int cpg = c / 32;
+    gn_targets_[x.p].push_back(dc_gn_target{acc, 0, 32, cpg, hw});
+    if (x2.p) gn_targets_[x2.p].push_back(dc_gn_target{acc, c1, 32, cpg, hw});
+    return acc;
+  }
+  const dc_gn_fuse* gnf(RB y) {
+    if (!fuse_gn_) return nullptr;
+    auto it = gn_fuse_.find(y.p);
+    if (it != gn_fuse_.end()) return it->second.get();
+    auto tg = gn_targets_.find(y.p);
+    if (tg == gn_targets_.end()) return nullptr;
+    if (tg->second.size() > 2) throw DcError(kErrArg, "GroupNorm statistics: more than two consumers");
+    auto g = std::make_unique<dc_gn_fuse>();
+    memset(g.get(), 0, sizeof(dc_gn_fuse));
+    g->mode = 1;
+    g->nt = (int)tg->second.size();
+    for (int k = 0; k < g->nt; ++k) g->t[k] = tg->second[k];
+    return (gn_fuse_[y.p] = std::move(g)).get();
+  }
+  void gn_fwd(RB x, int hw, int c, const NormW& n, bool silu, long long* acc, RB y, float* stats, RB x2 = RB(),
+              int c1 = 0) {
+    if (acc) ex_.groupnorm_acc(x, nb_, hw, c, n, silu, acc, y, stats, x2, c1);
+    else ex_.groupnorm(x, nb_, hw, c, n, silu, y, stats, x2, c1);
+  }
+  // (accumulator, dc_gn_fuse mode 2) of the conv producing dL/d(GroupNorm output)
+  std::pair<long long*, const dc_gn_fuse*> gn_bwd_fuse(RB x, int hw, int c, const NormW& n, bool silu,
+                                                        const float* stats, RB x2 = RB(), int c1 = 0) {
+    if (!gn_pays(hw, c, true)) return {nullptr, nullptr};
+    long long* acc = gn_acc();
+    auto g = std::make_unique<dc_gn_fuse>();
+    memset(g.get(), 0, sizeof(dc_gn_fuse));
+    g->mode = 2;
+    g->nt = 1;
+    g->t[0] = dc_gn_target{acc, 0, 32, c / 32, hw};
+    g->x = x.p;
+    g->ldx = x.ld;
+    g->x2 = x2.p;
+    g->ldx2 = x2.p ? x2.ld : 0;
+    g->c1 = c1;
+    g->stats = stats;
+    g->gamma = n.gamma;
+    g->beta = n.beta;
+    g->silu = silu ? 1 : 0;
+    gn_bwd_.push_back(std::move(g));
+    return {acc, gn_bwd_.back().get()};
+  }
+  void gn_bwd(RB x, int hw, int c, const NormW& n, bool silu, const float* stats, long long* acc, RB dy, RB dx,
+              RB x2 = RB(), int c1 = 0, RB add1 = RB(), RB add2 = RB()) {
+    if (acc) ex_.groupnorm_bwd_acc(x, nb_, hw, c, n, stats, acc, dy, dx, x2, c1, add1, add2);
+    else ex_.groupnorm_bwd(x, nb_, hw, c, n, silu, stats, dy, dx, x2, c1, add1, add2);
+  }
 
   RB buf(long rows, int cols) { return RB(mem_.alloc((size_t)rows * cols * 2), cols); }
   float* fbuf(long n) { return (float*)mem_.alloc((size_t)n * 4); }
@@ -616,14 +707,17 @@ class UNetPlan {
     RB sc = r.has_sc ? buf(P, cout) : RB();
     ResnetW* rp = &r;
     Exec& ex = ex_;
+    long long* acc1 = gn_consumer(x, cin, hh * ww, x2, c1);
+    long long* acc2 = gn_consumer(h1, cout, hh * ww);
     fwd_.push_back([=, &ex]() {
-      ex.groupnorm(x, nb, hh * ww, cin, rp->n1, true, g1, st1, x2, c1);
+      gn_fwd(x, hh * ww, cin, rp->n1, true, acc1, g1, st1, x2, c1);
       Exec::Conv a;
       a.x = g1; a.nb = nb; a.hin = hh; a.win = ww; a.cin = cin; a.hout = hh; a.wout = ww; a.cout = cout;
       a.w = rp->c1.wf; a.ktot = rp->c1.ktot_f; a.bias = rp->c1.bias; a.rowbias = rp->temb_table; a.rowbias_ld = cout;
       a.y = h1;
+      a.gn = gnf(h1);
       ex.conv(a);
-      ex.groupnorm(h1, nb, hh * ww, cout, rp->n2, true, g2, st2);
+      gn_fwd(h1, hh * ww, cout, rp->n2, true, acc2, g2, st2);
       RB res = x;
       if (rp->has_sc) {
         Exec::Conv s;
@@ -636,6 +730,7 @@ class UNetPlan {
       Exec::Conv b;
       b.x = g2; b.nb = nb; b.hin = hh; b.win = ww; b.cin = cout; b.hout = hh; b.wout = ww; b.cout = cout;
       b.w = rp->c2.wf; b.ktot = rp->c2.ktot_f; b.bias = rp->c2.bias; b.resid = res; b.y = out;
+      b.gn = gnf(out);
       ex.conv(b);
     });
     TapeEntry e;
@@ -664,8 +759,9 @@ class UNetPlan {
     RB f8 = buf(P, 8 * C), gg = buf(P, 4 * C), r3 = buf(P, C), out = buf(P, C);
     TransformerW* tp = &t;
     Exec& ex = ex_;
+    long long* acc0 = gn_consumer(x, C, T);
     fwd_.push_back([=, &ex]() {
-      ex.groupnorm(x, nb, T, C, tp->norm, false, n0, st0);
+      gn_fwd(x, T, C, tp->norm, false, acc0, n0, st0);
       ex.linear(n0, tp->proj_in.wf, tp->proj_in.cin, P, C, p, tp->proj_in.bias);
       DCK(dc_layernorm_fwd(p.p, p.ld, P, C, tp->ln1.eps, tp->ln1.gamma, tp->ln1.beta, l1.p, l1.ld, sl1, ex.stream));
       ex.linear(l1, tp->qkv.wf, tp->qkv.cin, P, 3 * C, qkv);
@@ -676,7 +772,8 @@ class UNetPlan {
       DCK(dc_layernorm_fwd(r2.p, r2.ld, P, C, tp->ln3.eps, tp->ln3.gamma, tp->ln3.beta, l3.p, l3.ld, sl3, ex.stream));
       ex.linear(l3, tp->ff1.wf, tp->ff1.cin, P, 8 * C, f8, tp->ff1.bias, RB(), nullptr, 0, 1, gg);
       ex.linear(gg, tp->ff2.wf, tp->ff2.cin, P, C, r3, tp->ff2.bias, r2);
-      ex.linear(r3, tp->proj_out.wf, tp->proj_out.cin, P, C, out, tp->proj_out.bias, x);
+      ex.linear(r3, tp->proj_out.wf, tp->proj_out.cin, P, C, out, tp->proj_out.bias, x, nullptr, 0, 0, RB(), RB(),
+                gnf(out));
     });
     TapeEntry e;
     e.kind = "transformer";
@@ -697,6 +794,7 @@ class UNetPlan {
       Exec::Conv a;
       a.x = x; a.nb = nb; a.hin = hh; a.win = ww; a.cin = c->cin; a.hout = ho; a.wout = wo; a.cout = c->cout;
       a.stride = 2; a.w = c->wf; a.ktot = c->ktot_f; a.bias = c->bias; a.y = out;
+      a.gn = gnf(out);
       ex.conv(a);
     });
     TapeEntry e;
@@ -719,6 +817,7 @@ class UNetPlan {
       Exec::Conv a;
       a.x = x; a.nb = nb; a.hin = hh; a.win = ww; a.cin = c->cin; a.hout = ho; a.wout = wo; a.cout = c->cout;
       a.mode = 1; a.w = c->wf; a.ktot = c->ktot_f; a.bias = c->bias; a.y = out;
+      a.gn = gnf(out);
       ex.conv(a);
     });
     TapeEntry e;
@@ -741,9 +840,11 @@ class UNetPlan {
       RB x8v = x8;
       const int H = h_, W = w_;
       fwd_.push_back([=, &ex]() {
+        if (fuse_gn_) ex.memset0(gn_arena_, gn_arena_bytes_);   // every accumulator of the step starts at zero
         Exec::Conv a;
         a.x = x8v; a.nb = nb; a.hin = H; a.win = W; a.cin = 8; a.hout = H; a.wout = W; a.cout = c0;
         a.w = n->conv_in.wf; a.ktot = n->conv_in.ktot_f; a.bias = n->conv_in.bias; a.y = h0;
+        a.gn = gnf(h0);
         ex.conv(a);
       });
       TapeEntry e;
@@ -796,8 +897,9 @@ class UNetPlan {
       UNetW* n = &net_;
       RB vout = v;
       const int H = h_, W = w_;
+      long long* acc_h = gn_consumer(xin, c0, H * W);
       fwd_.push_back([=, &ex]() {
-        ex.groupnorm(xin, nb, H * W, c0, n->norm_out, true, g, st);
+        gn_fwd(xin, H * W, c0, n->norm_out, true, acc_h, g, st);
         Exec::Conv a;
         a.x = g; a.nb = nb; a.hin = H; a.win = W; a.cin = c0; a.hout = H; a.wout = W; a.cout = 4;
         a.w = n->conv_out.wf; a.ktot = n->conv_out.ktot_f; a.bias = n->conv_out.bias; a.y = vout;
@@ -825,12 +927,14 @@ class UNetPlan {
         grad_of[x.p] = dx;
         float* st = d.f["st"];
         RB dvv = dv;
+        auto fb = gn_bwd_fuse(x, H * W, c0, n->norm_out, true, st);
         bwd_.push_back([=, &ex]() {
           Exec::Conv a;
           a.x = dvv; a.nb = nb; a.hin = H; a.win = W; a.cin = 8; a.hout = H; a.wout = W; a.cout = c0;
           a.w = n->conv_out.wd; a.ktot = n->conv_out.ktot_d; a.y = dg;
+          a.gn = fb.second;
           ex.conv(a);
-          ex.groupnorm_bwd(x, nb, H * W, c0, n->norm_out, true, st, dg, dx);
+          gn_bwd(x, H * W, c0, n->norm_out, true, st, fb.first, dg, dx);
         });
       } else if (d.kind == "up") {
         ConvW* cv = d.cv;
@@ -898,20 +1002,24 @@ class UNetPlan {
       if (e != extra_of.end()) extra = e->second;
     }
     Exec& ex = ex_;
+    auto f2 = gn_bwd_fuse(h1, hh * ww, cout, r->n2, true, st2);
+    auto f1 = gn_bwd_fuse(x, hh * ww, cin, r->n1, true, st1, x2, c1);
     bwd_.push_back([=, &ex]() {
       Exec::Conv a;
       a.x = dout; a.nb = nb; a.hin = hh; a.win = ww; a.cin = cout; a.hout = hh; a.wout = ww; a.cout = cout;
       a.w = r->c2.wd; a.ktot = r->c2.ktot_d; a.y = dg2;
+      a.gn = f2.second;
       ex.conv(a);
-      ex.groupnorm_bwd(h1, nb, hh * ww, cout, r->n2, true, st2, dg2, dh1);
+      gn_bwd(h1, hh * ww, cout, r->n2, true, st2, f2.first, dg2, dh1);
       Exec::Conv b;
       b.x = dh1; b.nb = nb; b.hin = hh; b.win = ww; b.cin = cout; b.hout = hh; b.wout = ww; b.cout = cin;
       b.w = r->c1.wd; b.ktot = r->c1.ktot_d; b.y = dg1;
+      b.gn = f1.second;
       ex.conv(b);
       if (!r->has_sc) {
-        ex.groupnorm_bwd(x, nb, hh * ww, cin, r->n1, true, st1, dg1, dx, x2, c1, dout, extra);
+        gn_bwd(x, hh * ww, cin, r->n1, true, st1, f1.first, dg1, dx, x2, c1, dout, extra);
       } else {
-        ex.groupnorm_bwd(x, nb, hh * ww, cin, r->n1, true, st1, dg1, dx, x2, c1, extra);
+        gn_bwd(x, hh * ww, cin, r->n1, true, st1, f1.first, dg1, dx, x2, c1, extra);
         Exec::Conv s;
         s.x = dout; s.nb = nb; s.hin = hh; s.win = ww; s.cin = cout; s.hout = hh; s.wout = ww; s.cout = cin;
         s.kh = 1; s.kw = 1; s.pad = 0; s.w = r->sc.wd; s.ktot = r->sc.ktot_d; s.resid = dx; s.y = dx;
@@ -937,6 +1045,7 @@ class UNetPlan {
     float *st0 = d.f["st0"], *sl1 = d.f["sl1"], *lse = d.f["lse"], *sl2 = d.f["sl2"], *probs = d.f["probs"],
           *sl3 = d.f["sl3"];
     Exec& ex = ex_;
+    auto f0 = gn_bwd_fuse(x, T, C, t->norm, false, st0);
     bwd_.push_back([=, &ex]() {
       ex.linear(dout, t->proj_out.wd, t->proj_out.cout, P, C, dr3);
       ex.linear(dr3, t->ff2.wd, t->ff2.cout, P, 4 * C, df, nullptr, RB(), nullptr, 0, 2, RB(), f8);
@@ -951,8 +1060,8 @@ class UNetPlan {
       ex.linear(dqkv, t->qkv.wd, t->qkv.cout, P, C, dl1);
       DCK(dc_layernorm_bwd(p.p, p.ld, P, C, t->ln1.gamma, sl1, dl1.p, dl1.ld, dp.p, dp.ld, dr1.p, dr1.ld,
                            ex.stream));
-      ex.linear(dp, t->proj_in.wd, t->proj_in.cout, P, C, dn0);
-      ex.groupnorm_bwd(x, nb, T, C, t->norm, false, st0, dn0, dx, RB(), 0, dout, extra);
+      ex.linear(dp, t->proj_in.wd, t->proj_in.cout, P, C, dn0, nullptr, RB(), nullptr, 0, 0, RB(), RB(), f0.second);
+      gn_bwd(x, T, C, t->norm, false, st0, f0.first, dn0, dx, RB(), 0, dout, extra);
     });
   }
 };

@@ -16,7 +16,7 @@ from pathlib import Path
 import torch
 
 from . import _lib
-from ._lib import ConvDesc, call
+from ._lib import ConvDesc, GnFuse, call
 
 BF16 = torch.bfloat16
 
@@ -142,8 +142,9 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
               cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
               c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
               y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None, geglu: int = 0,
-              y2=None, aux=None, rows=None):
-    """The dc_conv_desc of one conv_gemm call, its (algo, split) chosen (tuned table / nearest shape)."""
+              y2=None, aux=None, rows=None, gn: GnFuse | None = None):
+    """The dc_conv_desc of one conv_gemm call, its (algo, split) chosen (tuned table / nearest shape).
+    gn: fused GroupNorm statistics (include/dcamd.h dc_gn_fuse; the caller keeps it alive)."""
     d = ConvDesc()
     d.x = P(x)
     d.ldx = LD(x)
@@ -173,6 +174,8 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     d.ldaux = LD(aux)
     d.ws = ctx.ws.data_ptr() if splitk else None
     d.ws_bytes = ctx.ws_bytes if splitk else 0
+    if gn is not None:
+        d.gn = C.pointer(gn)
     if rows is not None:
         d.rows, d.nrows = rows[0].data_ptr(), int(rows[1])
         if algo is None:   # row counts vary per call: the library heuristic on nrows, not the tuned table
@@ -184,7 +187,8 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     return d
 
 
-HALO_FIRST = 23   # dc_conv_gemm algo ids >= this run the halo-tile direct 3x3 conv (conv_gemm.hip)
+HALO_FIRST, HALO_LAST = 23, 36   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv (conv_gemm_impl.h); ids
+# 1 .. 22 and 37 .. dc_conv_num_algos() are im2col tile variants
 
 
 def halo_eligible(d) -> bool:
@@ -209,14 +213,18 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     base = y.t.data_ptr() if isinstance(y, Slice) else y.data_ptr()
     dt = ConvDesc.from_buffer_copy(d)
     dt.y = tmp.data_ptr() + (d.y - base)
+    dt.gn = None   # candidates must not add to the GroupNorm accumulators
     nalg = _lib.load().dc_conv_num_algos()
     # im2col tiles: split-K 1..32, and stream-K over 256 / 512 / 768 blocks (splitk -1 / -2 / -3); halo tiles
     # (algos > HALO_FIRST - 1, stride-1 3x3 convs over whole 64-channel chunks only): input-chunk splits
-    cands = [(0, 0)] + [(a, s) for a in range(1, min(nalg, HALO_FIRST - 1) + 1)
-                        for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
+    gemm_ids = list(range(1, HALO_FIRST)) + list(range(HALO_LAST + 1, nalg + 1))
+    cands = [(0, 0)] + [(a, s) for a in gemm_ids for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
     if halo_eligible(d):
-        cands += [(a, s) for a in range(HALO_FIRST, nalg + 1) for s in (1, 2, 3, 4, 5, 8, 10, 16, 20)
+        cands += [(a, s) for a in range(HALO_FIRST, HALO_LAST + 1) for s in (1, 2, 3, 4, 5, 8, 10, 16, 20)
                   if s <= d.cin // 64]
+    if getattr(ctx, "tune_only", None):   # tools/tune_gemm.py --try: the committed choice against these algos only
+        cur = ctx.tune_only[1].get(conv_key(d))
+        cands = ([cur] if cur else []) + [c for c in cands if c[0] in ctx.tune_only[0]]
     best, best_t = (0, 0), float("inf")
     # DC_TUNE_COLD=1: every timed call starts with L2 and the Infinity Cache flushed (a 512 MiB write),
     # as the weights are in the sampler step (each is touched once per pass)
@@ -261,12 +269,12 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
 
 def linear(ctx: Ctx, x, w: torch.Tensor, rows: int, cout: int, y, bias=None, resid=None, rowbias=None,
            rowbias_ld: int = 0, act: int = 0, geglu: int = 0, y2=None, aux=None, algo: int | None = None,
-           nsplit: int | None = None):
+           nsplit: int | None = None, gn: GnFuse | None = None):
     """y[rows, cout] = x[rows, K] @ w[cout, K]^T (+ bias, + resid); geglu 1 / 2: the fused GEGLU
     epilogues of include/dcamd.h (y2 = h * gelu(gate); aux = interleaved pre-activation)."""
     return conv_gemm(ctx, x, w, nb=1, hin=1, win=rows, cin=w.shape[1], hout=1, wout=rows, cout=cout, kh=1, kw=1,
                      stride=1, pad=0, bias=bias, resid=resid, rowbias=rowbias, rowbias_ld=rowbias_ld, act=act, y=y,
-                     geglu=geglu, y2=y2, aux=aux, algo=algo, nsplit=nsplit)
+                     geglu=geglu, y2=y2, aux=aux, algo=algo, nsplit=nsplit, gn=gn)
 
 
 # ------------------------------------------------------------------------- norms
@@ -281,6 +289,51 @@ def groupnorm_bwd(ctx: Ctx, x, nb, hw, c, gamma, beta, silu, stats, dy, dx, x2=N
     call("dc_groupnorm_bwd", P(x), LD(x), P(x2), LD(x2), c1, nb, hw, c, groups, gamma.data_ptr(), beta.data_ptr(),
          int(silu), stats.data_ptr(), P(dy), LD(dy), P(dx), LD(dx), P(add1), LD(add1), P(add2), LD(add2),
          ctx.ws.data_ptr(), ctx.stream)
+    return dx
+
+
+def call_int(name: str, *args) -> int:
+    """A libdcamd query that returns a value rather than a status."""
+    return int(getattr(_lib.load(), name)(*args))
+
+
+def gn_acc_words(nb: int, groups: int = 32) -> int:
+    """int64 words of one fused-statistics accumulator (dc_gn_acc_bytes: replicas x frames x groups x 2 x 9)."""
+    return int(_lib.load().dc_gn_acc_bytes(nb, groups)) // 8
+
+
+def gn_fuse_fwd(targets) -> GnFuse:
+    """dc_gn_fuse mode 1 for an output feeding the GroupNorms ``targets`` [(acc, coff, groups, cpg, hw)]."""
+    g = GnFuse()
+    g.mode, g.nt = 1, len(targets)
+    for k, (acc, coff, groups, cpg, hw) in enumerate(targets):
+        g.t[k].acc, g.t[k].coff, g.t[k].groups, g.t[k].cpg, g.t[k].hw = acc.data_ptr(), coff, groups, cpg, hw
+    return g
+
+
+def gn_fuse_bwd(acc, groups, cpg, hw, x, stats, gamma, beta, silu, x2=None, c1=0) -> GnFuse:
+    """dc_gn_fuse mode 2: the output is dL/d(GroupNorm(x)(+SiLU)); the epilogue stores dy' and sums into acc."""
+    g = GnFuse()
+    g.mode, g.nt = 2, 1
+    g.t[0].acc, g.t[0].coff, g.t[0].groups, g.t[0].cpg, g.t[0].hw = acc.data_ptr(), 0, groups, cpg, hw
+    g.x, g.ldx, g.x2, g.ldx2, g.c1 = P(x), LD(x), P(x2), LD(x2), c1
+    g.stats, g.gamma, g.beta, g.silu = stats.data_ptr(), gamma.data_ptr(), beta.data_ptr(), int(silu)
+    return g
+
+
+def groupnorm_acc(ctx: Ctx, x, nb, hw, c, gamma, beta, eps, silu, acc, y, stats, x2=None, c1=0, groups=32):
+    """One-pass GroupNorm(+SiLU) from the statistics its producers accumulated (dc_groupnorm_fwd_acc)."""
+    call("dc_groupnorm_fwd_acc", P(x), LD(x), P(x2), LD(x2), c1, nb, hw, c, groups, eps, gamma.data_ptr(),
+         beta.data_ptr(), int(silu), acc.data_ptr(), P(y), LD(y), stats.data_ptr(), ctx.stream)
+    return y
+
+
+def groupnorm_bwd_acc(ctx: Ctx, x, nb, hw, c, gamma, stats, acc, dyp, dx, x2=None, c1=0, add1=None, add2=None,
+                      groups=32):
+    """GroupNorm input-gradient from the producer's dy' and accumulated sums (dc_groupnorm_bwd_acc)."""
+    call("dc_groupnorm_bwd_acc", P(x), LD(x), P(x2), LD(x2), c1, nb, hw, c, groups, gamma.data_ptr(),
+         stats.data_ptr(), acc.data_ptr(), P(dyp), LD(dyp), P(dx), LD(dx), P(add1), LD(add1), P(add2), LD(add2),
+         ctx.stream)
     return dx
 
 

@@ -9,6 +9,8 @@ hipGraph capture of one guided step needs.  Only the gradient w.r.t. the depth-l
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import ops
@@ -167,6 +169,20 @@ class UNetPlan:
         self.v = self.buf(P, 8)
         self.dv = self.buf(P, 8)
         self.gx = self.buf(P, 8)
+        # GroupNorm statistics fused into the producing convs (include/dcamd.h dc_gn_fuse; DC_GN_FUSE=0: the
+        # separate statistics passes).  One exact accumulator per GroupNorm and direction, all in one arena that
+        # the forward zero-fills first; a producer looks up the GroupNorms its output feeds (_gn_targets) at call
+        # time, since a skip tensor's up-block consumer is planned long after its producer.
+        self.fuse_gn = os.environ.get("DC_GN_FUSE", "1") != "0"
+        self.groups = net.cfg.norm_num_groups
+        n_res = sum(1 for _ in net.resnets())
+        n_tr = sum(len(b["attns"]) for b in net.down + net.up) + 1
+        n_gn = 2 * (2 * n_res + n_tr + 1)
+        self._gn_words = ops.gn_acc_words(nb, self.groups)
+        self.gn_arena = torch.zeros(n_gn * self._gn_words, dtype=torch.int64, device=dev)
+        self._gn_next = 0
+        self._gn_targets: dict = {}   # id(tensor) -> [(acc, coff, groups, cpg, hw)]
+        self._gn_fuse: dict = {}      # id(tensor) -> ops.GnFuse, built at the first call
         self._build_forward()
         self.bwd: list = []
         self._build_backward()
@@ -182,6 +198,63 @@ class UNetPlan:
         self.saved.append(t)
         return t
 
+    # ------------------------------------------------------------------ fused GroupNorm statistics
+    def _gn_acc(self) -> torch.Tensor:
+        i = self._gn_next
+        self._gn_next += 1
+        return self.gn_arena[i * self._gn_words:(i + 1) * self._gn_words]
+
+    def _gn_pays(self, hw, c, backward):
+        return self.fuse_gn and bool(ops.call_int("dc_gn_fuse_pays", hw, c, self.groups, int(backward)))
+
+    def _gn_consumer(self, x, c, hw, x2=None, c1=0):
+        """A forward GroupNorm over x (channels >= c1 from x2): its accumulator, registered with the producers (None:
+        the separate-pass GroupNorm, where fusing does not pay, dc_gn_fuse_pays)."""
+        if not self._gn_pays(hw, c, False):
+            return None
+        acc = self._gn_acc()
+        cpg = c // self.groups
+        self._gn_targets.setdefault(id(x), []).append((acc, 0, self.groups, cpg, hw))
+        if x2 is not None:
+            self._gn_targets.setdefault(id(x2), []).append((acc, c1, self.groups, cpg, hw))
+        return acc
+
+    def _gnf(self, y):
+        """dc_gn_fuse (mode 1) for a conv writing y, or None when no GroupNorm reads y."""
+        if not self.fuse_gn:
+            return None
+        g = self._gn_fuse.get(id(y))
+        if g is None:
+            tg = self._gn_targets.get(id(y))
+            if tg is None:
+                return None
+            g = self._gn_fuse[id(y)] = ops.gn_fuse_fwd(tg)
+        return g
+
+    def _gn_fwd(self, x, hw, c, norm, silu, acc, y, stats, x2=None, c1=0):
+        if acc is not None:
+            ops.groupnorm_acc(self.ctx, x, self.nb, hw, c, norm.gamma, norm.beta, norm.eps, silu, acc, y, stats,
+                              x2=x2, c1=c1, groups=self.groups)
+        else:
+            ops.groupnorm(self.ctx, x, self.nb, hw, c, norm.gamma, norm.beta, norm.eps, silu, y, stats, x2=x2, c1=c1,
+                          groups=self.groups)
+
+    def _gn_bwd_fuse(self, x, hw, c, norm, silu, stats, x2=None, c1=0):
+        """(accumulator, dc_gn_fuse mode 2) for the conv producing dL/d(GroupNorm output), or (None, None)."""
+        if not self._gn_pays(hw, c, True):
+            return None, None
+        acc = self._gn_acc()
+        return acc, ops.gn_fuse_bwd(acc, self.groups, c // self.groups, hw, x, stats, norm.gamma, norm.beta, silu,
+                                    x2=x2, c1=c1)
+
+    def _gn_bwd(self, x, hw, c, norm, silu, stats, acc, dy, dx, x2=None, c1=0, add1=None, add2=None):
+        if acc is not None:
+            ops.groupnorm_bwd_acc(self.ctx, x, self.nb, hw, c, norm.gamma, stats, acc, dy, dx, x2=x2, c1=c1,
+                                  add1=add1, add2=add2, groups=self.groups)
+        else:
+            ops.groupnorm_bwd(self.ctx, x, self.nb, hw, c, norm.gamma, norm.beta, silu, stats, dy, dx, x2=x2, c1=c1,
+                              add1=add1, add2=add2, groups=self.groups)
+
     # ------------------------------------------------------------------ forward
     def _resnet(self, r: ResnetW, x, hw, x2=None, c1=0):
         ctx, nb = self.ctx, self.nb
@@ -195,20 +268,21 @@ class UNetPlan:
         g2 = self.buf(P, cout)
         out = self.buf(P, cout)
         sc = self.buf(P, cout) if r.shortcut is not None else None
+        acc1 = self._gn_consumer(x, cin, hh * ww, x2=x2, c1=c1)
+        acc2 = self._gn_consumer(h1, cout, hh * ww)
 
         def f():
-            ops.groupnorm(ctx, x, nb, hh * ww, cin, r.norm1.gamma, r.norm1.beta, r.norm1.eps, True, g1, st1, x2=x2,
-                          c1=c1)
+            self._gn_fwd(x, hh * ww, cin, r.norm1, True, acc1, g1, st1, x2=x2, c1=c1)
             ops.conv_gemm(ctx, g1, r.conv1.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
-                          bias=r.conv1.bias, rowbias=r.temb_table, rowbias_ld=cout, y=h1)
-            ops.groupnorm(ctx, h1, nb, hh * ww, cout, r.norm2.gamma, r.norm2.beta, r.norm2.eps, True, g2, st2)
+                          bias=r.conv1.bias, rowbias=r.temb_table, rowbias_ld=cout, y=h1, gn=self._gnf(h1))
+            self._gn_fwd(h1, hh * ww, cout, r.norm2, True, acc2, g2, st2)
             res = x
             if r.shortcut is not None:
                 ops.conv_gemm(ctx, x, r.shortcut.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
                               kh=1, kw=1, pad=0, x2=x2, c1=c1, bias=r.shortcut.bias, y=sc)
                 res = sc
             ops.conv_gemm(ctx, g2, r.conv2.wf, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout,
-                          bias=r.conv2.bias, resid=res, y=out)
+                          bias=r.conv2.bias, resid=res, y=out, gn=self._gnf(out))
 
         self.fwd.append(f)
         self.tape.append(("resnet", dict(r=r, x=x, x2=x2, c1=c1, hw=hw, st1=st1, h1=h1, st2=st2, out=out)))
@@ -240,9 +314,10 @@ class UNetPlan:
         gg = self.buf(P, 4 * C)
         r3 = self.buf(P, C)
         out = self.buf(P, C)
+        acc0 = self._gn_consumer(x, C, T)
 
         def f():
-            ops.groupnorm(ctx, x, nb, T, C, t.norm.gamma, t.norm.beta, t.norm.eps, False, n0, st0)
+            self._gn_fwd(x, T, C, t.norm, False, acc0, n0, st0)
             ops.linear(ctx, n0, t.proj_in.wf, P, C, p, bias=t.proj_in.bias)
             ops.layernorm(ctx, p, P, C, t.ln1.gamma, t.ln1.beta, t.ln1.eps, l1, sl1)
             ops.linear(ctx, l1, t.qkv.wf, P, 3 * C, qkv)
@@ -253,7 +328,7 @@ class UNetPlan:
             ops.layernorm(ctx, r2, P, C, t.ln3.gamma, t.ln3.beta, t.ln3.eps, l3, sl3)
             ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias, geglu=1, y2=gg)   # + GEGLU
             ops.linear(ctx, gg, t.ff2.wf, P, C, r3, bias=t.ff2.bias, resid=r2)
-            ops.linear(ctx, r3, t.proj_out.wf, P, C, out, bias=t.proj_out.bias, resid=x)
+            ops.linear(ctx, r3, t.proj_out.wf, P, C, out, bias=t.proj_out.bias, resid=x, gn=self._gnf(out))
 
         self.fwd.append(f)
         self.tape.append(("transformer", dict(t=t, x=x, hw=hw, st0=st0, p=p, sl1=sl1, qkv=qkv, o=o, lse=lse, r1=r1,
@@ -268,7 +343,7 @@ class UNetPlan:
 
         def f():
             ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, stride=2,
-                          bias=cv.bias, y=out)
+                          bias=cv.bias, y=out, gn=self._gnf(out))
 
         self.fwd.append(f)
         self.tape.append(("down", dict(cv=cv, x=x, hw=hw, ohw=(ho, wo), out=out)))
@@ -282,7 +357,7 @@ class UNetPlan:
 
         def f():
             ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, mode=1,
-                          bias=cv.bias, y=out)
+                          bias=cv.bias, y=out, gn=self._gnf(out))
 
         self.fwd.append(f)
         self.tape.append(("up", dict(cv=cv, x=x, hw=hw, ohw=ohw, out=out)))
@@ -297,8 +372,10 @@ class UNetPlan:
         x8 = self.x8
 
         def f_in():
+            if self.fuse_gn:   # every accumulator of the step (forward and backward) starts at zero
+                ops.memset(ctx, self.gn_arena)
             ops.conv_gemm(ctx, x8, net.conv_in.wf, nb=nb, hin=self.h, win=self.w, cin=8, hout=self.h, wout=self.w,
-                          cout=c0, bias=net.conv_in.bias, y=h0)
+                          cout=c0, bias=net.conv_in.bias, y=h0, gn=self._gnf(h0))
 
         self.fwd.append(f_in)
         self.tape.append(("conv_in", dict(out=h0)))
@@ -335,10 +412,10 @@ class UNetPlan:
         g = self.buf(P, c0)
         st = self.fbuf(nb, 32, 2)
         xin = x
+        acc_h = self._gn_consumer(xin, c0, self.h * self.w)
 
         def f_out():
-            ops.groupnorm(ctx, xin, nb, self.h * self.w, c0, net.norm_out.gamma, net.norm_out.beta, net.norm_out.eps,
-                          True, g, st)
+            self._gn_fwd(xin, self.h * self.w, c0, net.norm_out, True, acc_h, g, st)
             ops.conv_gemm(ctx, g, net.conv_out.wf, nb=nb, hin=self.h, win=self.w, cin=c0, hout=self.h, wout=self.w,
                           cout=4, bias=net.conv_out.bias, y=self.v)
 
@@ -361,12 +438,12 @@ class UNetPlan:
                 dx = self.buf(P, c0)
                 grad_of[id(x)] = dx
                 st = d["st"]
+                accb, gnb = self._gn_bwd_fuse(x, dev_h * dev_w, c0, net.norm_out, True, st)
 
-                def b(x=x, dg=dg, dx=dx, st=st, c0=c0):
+                def b(x=x, dg=dg, dx=dx, st=st, c0=c0, accb=accb, gnb=gnb):
                     ops.conv_gemm(ctx, self.dv, net.conv_out.wd, nb=nb, hin=dev_h, win=dev_w, cin=8, hout=dev_h,
-                                  wout=dev_w, cout=c0, y=dg)
-                    ops.groupnorm_bwd(ctx, x, nb, dev_h * dev_w, c0, net.norm_out.gamma, net.norm_out.beta, True,
-                                      st, dg, dx)
+                                  wout=dev_w, cout=c0, y=dg, gn=gnb)
+                    self._gn_bwd(x, dev_h * dev_w, c0, net.norm_out, True, st, accb, dg, dx)
 
                 bwd.append(b)
             elif kind == "up":
@@ -428,16 +505,19 @@ class UNetPlan:
             grad_of[id(x)] = dx
             extra = extra_of.get(id(x))
 
+        acc2, gn2 = self._gn_bwd_fuse(h1, hh * ww, cout, r.norm2, True, st2)
+        acc1, gn1 = self._gn_bwd_fuse(x, hh * ww, cin, r.norm1, True, st1, x2=x2, c1=c1)
+
         def b():
-            ops.conv_gemm(ctx, dout, r.conv2.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout, y=dg2)
-            ops.groupnorm_bwd(ctx, h1, nb, hh * ww, cout, r.norm2.gamma, r.norm2.beta, True, st2, dg2, dh1)
-            ops.conv_gemm(ctx, dh1, r.conv1.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin, y=dg1)
+            ops.conv_gemm(ctx, dout, r.conv2.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout, y=dg2,
+                          gn=gn2)
+            self._gn_bwd(h1, hh * ww, cout, r.norm2, True, st2, acc2, dg2, dh1)
+            ops.conv_gemm(ctx, dh1, r.conv1.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin, y=dg1,
+                          gn=gn1)
             if r.shortcut is None:
-                ops.groupnorm_bwd(ctx, x, nb, hh * ww, cin, r.norm1.gamma, r.norm1.beta, True, st1, dg1, dx,
-                                  x2=x2, c1=c1, add1=dout, add2=extra)
+                self._gn_bwd(x, hh * ww, cin, r.norm1, True, st1, acc1, dg1, dx, x2=x2, c1=c1, add1=dout, add2=extra)
             else:
-                ops.groupnorm_bwd(ctx, x, nb, hh * ww, cin, r.norm1.gamma, r.norm1.beta, True, st1, dg1, dx,
-                                  x2=x2, c1=c1, add1=extra)
+                self._gn_bwd(x, hh * ww, cin, r.norm1, True, st1, acc1, dg1, dx, x2=x2, c1=c1, add1=extra)
                 ops.conv_gemm(ctx, dout, r.shortcut.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin,
                               kh=1, kw=1, pad=0, resid=dx, y=dx)
 
@@ -468,6 +548,8 @@ class UNetPlan:
         st0, p, sl1, qkv, o, lse = d["st0"], d["p"], d["sl1"], d["qkv"], d["o"], d["lse"]
         r1, r2, sl2, probs, sl3, f8 = d["r1"], d["r2"], d["sl2"], d["probs"], d["sl3"], d["f8"]
 
+        acc0, gn0 = self._gn_bwd_fuse(x, T, C, t.norm, False, st0)
+
         def b():
             ops.linear(ctx, dout, t.proj_out.wd, P, C, dr3)
             ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, df, geglu=2, aux=f8)   # + GEGLU backward
@@ -478,9 +560,8 @@ class UNetPlan:
             ops.attn_bwd(ctx, qkv, o, do, lse, nb, T, H, delta, dqkv)
             ops.linear(ctx, dqkv, t.qkv.wd, P, C, dl1)
             ops.layernorm_bwd(ctx, p, P, C, t.ln1.gamma, sl1, dl1, dp, add=dr1)
-            ops.linear(ctx, dp, t.proj_in.wd, P, C, dn0)
-            ops.groupnorm_bwd(ctx, x, nb, T, C, t.norm.gamma, t.norm.beta, False, st0, dn0, dx, add1=dout,
-                              add2=extra)
+            ops.linear(ctx, dp, t.proj_in.wd, P, C, dn0, gn=gn0)
+            self._gn_bwd(x, T, C, t.norm, False, st0, acc0, dn0, dx, add1=dout, add2=extra)
 
         return b
 

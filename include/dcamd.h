@@ -32,6 +32,43 @@ const char* dc_build_id(void);
  *       2 transposed stride-2 gather (input-gradient of a stride-2 3x3 conv, Downsample2D).
  * Epilogue order: acc + bias -> (+ rowbias[*rowbias_idx]) -> (+ resid) -> relu? -> (* [mask > 0]).
  */
+/* GroupNorm statistics fused into the epilogue of the conv / linear that produces the normalised tensor
+ * (diffusers ResnetBlock2D norm1 / norm2, Transformer2DModel.norm, conv_norm_out: every GroupNorm input of the
+ * UNet is a conv or linear output, and so is every GroupNorm output-gradient).  The sums go into exact
+ * accumulators of dc_gn_acc_bytes(nb, groups) bytes (zero-filled before the producers run): per (frame, group)
+ * two quantities, each an integer of 8 32-bit limbs (LSB 2^-120) plus a non-finite count, to which every fp32
+ * contribution is added with integer atomics -- the sums are exact, so they do not depend on tile order or
+ * arrival order (bitwise reproducible).  dc_groupnorm_fwd_acc / dc_groupnorm_bwd_acc then normalise in one pass.
+ *   mode 1 (forward): (sum y, sum y^2) of the stored bf16 outputs into t[0 .. nt-1] (one output may be both the
+ *          direct input of one GroupNorm and the skip half (coff = c1) of an up-block concat);
+ *   mode 2 (backward): the output is dL/d(GroupNorm(+SiLU) output); with the GroupNorm input x (x2: channels
+ *          >= c1), its forward stats [nb][groups][2] (mean, rstd), gamma, beta the epilogue stores
+ *          dy' = bf16(dy * silu'(bf16(xhat gamma + beta))) (silu; else dy) and adds (sum gamma dy',
+ *          sum gamma dy' xhat) into t[0].
+ * Frames are hw output rows each (the row index of a linear over nb * hw token rows works the same way). */
+typedef struct dc_gn_target {
+  long long* acc;
+  int coff;         /* channel offset of this output inside the normalised tensor */
+  int groups, cpg;
+  int hw;
+} dc_gn_target;
+typedef struct dc_gn_fuse {
+  int mode;         /* 1 forward, 2 backward */
+  int nt;           /* targets used (1 or 2; mode 2: 1) */
+  dc_gn_target t[2];
+  const void* x;
+  const void* x2;
+  int ldx, ldx2, c1;
+  const float* stats;
+  const float* gamma;
+  const float* beta;
+  int silu;
+} dc_gn_fuse;
+long long dc_gn_acc_bytes(int nb, int groups);
+/* 1 where the fused statistics pay for a GroupNorm of hw pixels x c channels (forward / backward): not where the
+ * single-launch GroupNorm (one block per group, levels 2-3 of the UNet) runs it.  Both hosts plan with it. */
+int dc_gn_fuse_pays(int hw, int c, int groups, int backward);
+
 typedef struct dc_conv_desc {
   const void* x;   /* bf16 [nb*hin*win][ldx] */
   const void* x2;  /* optional second source for channels >= c1 (skip concat) */
@@ -70,6 +107,8 @@ typedef struct dc_conv_desc {
    * output rows) are computed and written; the others are left untouched (no GEGLU epilogue) */
   const int* rows;
   int nrows;
+  /* optional fused GroupNorm statistics (above; NULL: none).  Needs cout % 8 == 0, no row list, no GEGLU. */
+  const dc_gn_fuse* gn;
 } dc_conv_desc;
 
 int dc_conv_num_algos(void);
@@ -87,6 +126,16 @@ int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2, int c1, i
                      const float* gamma, const float* beta, int silu, const float* stats, const void* dy, int lddy,
                      void* dx, int lddx, const void* add1, int ldadd1, const void* add2, int ldadd2, float* ws,
                      void* stream);
+/* one-pass GroupNorm from the fused statistics (dc_gn_fuse): acc as filled by the producers of x (and x2).
+ * fwd: y = GN(x)(+SiLU), stats [nb][groups][2] (mean, rstd) written for the backward;
+ * bwd: dyp = the producer's stored dy' (mode 2), dx = rstd (gamma dy' - mean_a - xhat mean_b) (+ add1)(+ add2). */
+int dc_groupnorm_fwd_acc(const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c, int groups,
+                         float eps, const float* gamma, const float* beta, int silu, const long long* acc, void* y,
+                         int ldy, float* stats, void* stream);
+int dc_groupnorm_bwd_acc(const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c, int groups,
+                         const float* gamma, const float* stats, const long long* acc, const void* dyp, int lddy,
+                         void* dx, int lddx, const void* add1, int ldadd1, const void* add2, int ldadd2,
+                         void* stream);
 int dc_layernorm_fwd(const void* x, int ldx, long long rows, int c, float eps, const float* gamma, const float* beta,
                      void* y, int ldy, float* stats, void* stream);
 int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, const float* gamma, const float* stats,

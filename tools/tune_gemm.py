@@ -6,6 +6,7 @@ Runs one eager guided call per workload with Ctx.tune on (each new shape is time
 algos x split-K on its real operands) and writes the table that ops.load_tuned() reads.
 
 Usage: python tools/tune_gemm.py [--workloads c2:1 c2:8 c4:1 c4:8 c5:1] [--out depth_completion_amd/tuned_gfx950.json]
+       [--try 37 38 ...]  (the committed choices against new variants only)
   workload:batch -- c2 / c3: 768x576, 500 uniform points; c4: 1216x352, 64-beam rows; c5: 1600x900, 3000
   points, run as the 10-seed ensemble (one batch-10 call per frame, the shapes C5 launches)
 """
@@ -30,6 +31,9 @@ def main():
     ap.add_argument("--retune-3x3", action="store_true",
                     help="re-time the stride-1 3x3 shapes with cin % 64 == 0 (the halo-kernel contract) over every "
                          "variant, keep the committed choice of every other shape")
+    ap.add_argument("--try", dest="try_algos", type=int, nargs="+",
+                    help="re-time every shape of the workloads: its committed choice against these algo ids (all "
+                         "their splits) only; shapes outside the workloads keep their entries")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     pipe = MarigoldDepthCompletionPipeline(synthetic.unet_state_dict(MARIGOLD_V1, 11), synthetic.taesd_state_dict(12),
@@ -42,6 +46,10 @@ def main():
                 if not (k[8] == 3 and k[9] == 1 and k[4] % 64 == 0 and k[0] in (0, 1))}
         print(f"re-tuning {len(pipe.ctx.algo_cache) - len(keep)} 3x3 shapes", flush=True)
         pipe.ctx.algo_cache = keep
+    committed = dict(pipe.ctx.algo_cache)
+    if args.try_algos:
+        pipe.ctx.tune_only = (set(args.try_algos), committed)
+        pipe.ctx.algo_cache = {}
     pipe.ctx.tune = True
     shapes = {"c2": (576, 768, 500, "uniform"), "c3": (576, 768, 500, "uniform"), "c4": (352, 1216, 0, "beams"),
               "c5": (900, 1600, 3000, "uniform")}
@@ -59,6 +67,10 @@ def main():
         torch.cuda.synchronize()
         print(f"{wl}: {len(pipe.ctx.algo_cache) - n0} new shapes tuned", flush=True)
         ops.save_tuned(pipe.ctx.algo_cache, args.out)   # keep what is done if a later workload is cut off
+    if args.try_algos:
+        changed = sum(1 for k, v in pipe.ctx.algo_cache.items() if committed.get(k) != v)
+        print(f"--try {args.try_algos}: {changed} of {len(pipe.ctx.algo_cache)} re-timed shapes changed", flush=True)
+        pipe.ctx.algo_cache = {**committed, **pipe.ctx.algo_cache}
     ops.save_tuned(pipe.ctx.algo_cache, args.out)
     for k, v in sorted(pipe.ctx.algo_cache.items()):
         print(k, v)
