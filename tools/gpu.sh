@@ -7,6 +7,7 @@
 # first failing step (set -e): nothing else touches the GPU after a fault, abort or timeout.
 # Steps:
 #   tests[=<pytest -k expr>]   GPU suite (or the selected tests), -s output kept (printed errors)
+#   file=<test file(s)>        the GPU tests of these files
 #   smoke                      __graft_entry__.smoke()
 #   c2 | c2cpu                 C2 bench line (c2cpu: with the CPU baseline)
 #   c3 | c4 | c4b8 | c5        C3 batch 8, C4 KITTI 64-beam (batch 1 / 8), C5 10-seed ensemble bench lines
@@ -32,6 +33,10 @@ for step in "$@"; do
     tests=*)
       timeout -k 10 1200 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread -k "${step#tests=}" \
         > "$out/gputest_$n.log" 2>&1 ;;
+    file=*)
+      # shellcheck disable=SC2086
+      timeout -k 10 1200 python -u -m pytest ${step#file=} -m gpu -v -s --timeout 600 --timeout-method thread \
+        > "$out/gputest_$n.log" 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 ;;
     c2)
@@ -56,13 +61,16 @@ for step in "$@"; do
     trace3)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace3" -o run --output-format csv -- \
         python3 bench.py --batch 8 --steps 1 --warmup 1 --no-cpu-baseline > "$out/trace3_bench.json" 2> "$out/trace3.err" ;;
-    pmc)
-      timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex conv_gemm -d "$out/pmc_fetch" -o run \
-        --output-format csv -- python3 bench.py --no-graph --steps 1 --warmup 0 --no-cpu-baseline --denoise-steps 4 \
-        > "$out/pmc_fetch.json" 2> "$out/pmc_fetch.err"
-      timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex conv_gemm -d "$out/pmc_write" -o run \
-        --output-format csv -- python3 bench.py --no-graph --steps 1 --warmup 0 --no-cpu-baseline --denoise-steps 4 \
-        > "$out/pmc_write.json" 2> "$out/pmc_write.err" ;;
+    pmc|pmc8)
+      # FETCH_SIZE, WRITE_SIZE and the MFMA-busy pass over the conv kernels (im2col and halo), eager step, 4 denoise
+      # steps; each pass its own run (rocprofv3 does not split counters over passes)
+      b=1; [ "$step" = pmc8 ] && b=8
+      for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE:mfma"; do
+        # shellcheck disable=SC2086
+        timeout -s KILL 180 rocprofv3 --pmc ${pass%%:*} --kernel-include-regex "conv_(gemm|halo)_kernel" \
+          -d "$out/pmc${b}_${pass##*:}" -o run --output-format csv -- python3 bench.py --no-graph --steps 1 --warmup 0 \
+          --no-cpu-baseline --denoise-steps 4 --batch $b > "$out/pmc${b}_${pass##*:}.json" 2> "$out/pmc${b}_${pass##*:}.err"
+      done ;;
     stepprof)
       timeout -k 10 300 rocprofv3 --kernel-trace -d "$out/steptrace" -o run --output-format csv -- \
         python3 tools/step_profile.py --out "$out/descs.json" > "$out/stepprof.log" 2>&1
