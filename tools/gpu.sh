@@ -13,7 +13,7 @@
 #   c3 | c4 | c4b8 | c5        C3 batch 8, C4 KITTI 64-beam (batch 1 / 8), C5 10-seed ensemble bench lines
 #   trace                      rocprofv3 --kernel-trace --stats of a short C2 bench
 #   trace3                     the same for C3 (batch 8)
-#   pmc                        FETCH_SIZE and WRITE_SIZE passes over the conv kernel (eager C2, 4 denoise steps)
+#   pmc | pmc8                 FETCH_SIZE, WRITE_SIZE, MFMA-busy passes over the conv kernels (eager C2 / C3, 4 steps)
 #   breakdown[=<batch>]        per-shape conv breakdown of one guided step (tools/conv_breakdown.py)
 #   stepprof                   per-shape conv time inside the graph-replayed step (tools/step_profile.py)
 #   py=<script args>           any repo python script (e.g. py=tools/gemm_one.py --m 6912)
