@@ -16,11 +16,11 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libdcamd.so"
 OBJ_DIR = PKG / "build_obj"
-SOURCES = ["conv_gemm.hip", "conv_gemm_gn.hip", "conv_gemm_gnb.hip", "norms.hip", "attention.hip", "crossattn.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
+SOURCES = ["conv_gemm.hip", "conv_skinny9.hip", "conv_skinny1.hip", "conv_gemm_gn.hip", "conv_gemm_gnb.hip", "norms.hip", "attention.hip", "crossattn.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
            "rowsets.hip", "ensemble.hip", "host_tables.cpp", "session.cpp", "version.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DC_OFFLOAD_ARCH", "gfx950")
-HEADERS = [CSRC / h for h in ("common.h", "gn_acc.h", "conv_gemm_impl.h", "json_mini.h", "safetensors_mini.h")] + \
+HEADERS = [CSRC / h for h in ("common.h", "gn_acc.h", "conv_gemm_impl.h", "conv_skinny.h", "json_mini.h", "safetensors_mini.h")] + \
     [PKG.parent / "include" / "dcamd.h"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
@@ -39,6 +39,19 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def _includes(src: Path, seen: set | None = None) -> set:
+    """The repo headers a source includes, transitively (#include "..."): a header edit rebuilds only its users."""
+    seen = set() if seen is None else seen
+    for line in src.read_text(errors="ignore").splitlines():
+        line = line.strip()
+        if line.startswith("#include \""):
+            h = (src.parent / line.split('"')[1]).resolve()
+            if h.exists() and h not in seen:
+                seen.add(h)
+                _includes(h, seen)
+    return seen
+
+
 def _needs(obj: Path, deps: list[Path]) -> bool:
     if not obj.exists():
         return True
@@ -55,7 +68,7 @@ def build(verbose: bool = False, force: bool = False) -> Path:
         s = CSRC / src
         o = OBJ_DIR / (src + ".o")
         extra = []
-        deps = [s, *headers]
+        deps = [s, *_includes(s)]
         if src == "version.hip":   # carries the build id: rebuilt whenever any source changes
             extra = [f'-DDC_BUILD_ID="{bid}"']
             deps = source_files()

@@ -2,7 +2,14 @@
 // are in conv_gemm_impl.h; the fused GroupNorm-statistics instantiations are compiled in conv_gemm_gn.hip / conv_gemm_gnb.hip.
 #include "conv_gemm_impl.h"
 
-extern "C" int dc_conv_num_algos(void) { return kNumAll; }
+namespace {
+#include "conv_skinny.h"
+}  // namespace
+int conv_launch_skinny9(int i, ConvGemmParams& p, int splits, hipStream_t s);
+int conv_launch_skinny1(int i, ConvGemmParams& p, int splits, hipStream_t s);
+
+// external algo ids: 1 .. kNumAll im2col / halo variants (conv_gemm_impl.h), then the weight-streaming skinny variants
+extern "C" int dc_conv_num_algos(void) { return kNumAll + kNumSkinny; }
 
 extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (!d || !d->x || !d->w || !d->y) return DC_ERR_ARG;
@@ -51,7 +58,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
-  if (d->algo < 0 || d->algo > kNumAll || d->splitk < -4) return DC_ERR_ARG;
+  if (d->algo < 0 || d->algo > kNumAll + kNumSkinny || d->splitk < -4) return DC_ERR_ARG;
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;
@@ -111,6 +118,14 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
+  if (algo > kNumAll) {
+    const int si = algo - kNumAll - 1;
+    if (skinny_eligible(p, si))
+      return kSkinnyAlgos[si].kt == 9 ? conv_launch_skinny9(si, p, splits <= 0 ? 1 : splits, s)
+                                      : conv_launch_skinny1(si, p, splits <= 0 ? 1 : splits, s);
+    algo = 0;   // a skinny choice carried to a shape outside its contract (nearest-shape pick): im2col heuristic
+    splits = 0;
+  }
   if (algo_is_halo(algo)) {
     if (halo_eligible(p)) {
       const int hi = algo - kNumBase - 1;

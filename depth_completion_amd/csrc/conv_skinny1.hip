@@ -1,0 +1,11 @@
+// The weight-streaming skinny conv / linear kernels with 1 tap (conv_skinny.h); their own translation unit
+// so that the variants compile in parallel with the rest of dc_conv_gemm.
+#include "conv_gemm_impl.h"
+
+namespace {
+#include "conv_skinny.h"
+}  // namespace
+
+int conv_launch_skinny1(int i, ConvGemmParams& p, int splits, hipStream_t s) {
+  return launch_skinny_idx<1>(i, p, splits, s);
+}

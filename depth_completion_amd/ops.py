@@ -188,7 +188,10 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
 
 
 HALO_FIRST, HALO_LAST = 23, 36   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv (conv_gemm_impl.h); ids
-# 1 .. 22 and 37 .. dc_conv_num_algos() are im2col tile variants
+# 1 .. 22 and 37 .. 42 are im2col tile variants, SKINNY_FIRST .. dc_conv_num_algos() the weight-streaming skinny
+# conv / linear variants (conv_skinny.h)
+IM2COL_LAST, SKINNY_FIRST = 42, 43
+SKINNY_TAPS = (9, 9, 9, 9, 9, 1, 1, 1, 1, 1, 1, 1)   # taps of skinny variant SKINNY_FIRST + i (conv_skinny.h kSkinnyAlgos)
 
 
 def halo_eligible(d) -> bool:
@@ -198,6 +201,20 @@ def halo_eligible(d) -> bool:
             and not d.geglu and d.mode in (0, 1) and d.ktot == 9 * d.cin
             and (d.mode == 1 or (d.hin == d.hout and d.win == d.wout))
             and (not d.x2 or d.c1 % 64 == 0))
+
+
+def skinny_eligible(d) -> bool:
+    """Shapes the weight-streaming skinny variants serve (conv_skinny.h skinny_eligible, before the per-variant
+    chunk-group condition): the halo contract, or a 1x1 / linear over whole 64-channel chunks, with no fused
+    GroupNorm statistics; tuned only for the few-pixel layers (at most 512 output pixels: UNet levels 2-3 at batch 1,
+    where dc_gn_fuse_pays keeps the separate GroupNorm -- the first, tuning call of a shape runs before its GroupNorm
+    consumers register, so a fused-statistics conv looks unfused there and the variant would fall back in the step)."""
+    if d.gn or d.nb * d.hout * d.wout > 512:
+        return False
+    if d.kh == 1 and d.kw == 1:
+        return (d.stride == 1 and d.pad == 0 and d.mode == 0 and d.cin % 64 == 0 and d.ktot == d.cin and not d.rows
+                and not d.geglu and d.hin == d.hout and d.win == d.wout and (not d.x2 or d.c1 % 64 == 0))
+    return halo_eligible(d)
 
 
 def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
@@ -217,11 +234,16 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     nalg = _lib.load().dc_conv_num_algos()
     # im2col tiles: split-K 1..32, and stream-K over 256 / 512 / 768 blocks (splitk -1 / -2 / -3); halo tiles
     # (algos > HALO_FIRST - 1, stride-1 3x3 convs over whole 64-channel chunks only): input-chunk splits
-    gemm_ids = list(range(1, HALO_FIRST)) + list(range(HALO_LAST + 1, nalg + 1))
+    gemm_ids = list(range(1, HALO_FIRST)) + list(range(HALO_LAST + 1, IM2COL_LAST + 1))
     cands = [(0, 0)] + [(a, s) for a in gemm_ids for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
     if halo_eligible(d):
         cands += [(a, s) for a in range(HALO_FIRST, HALO_LAST + 1) for s in (1, 2, 3, 4, 5, 8, 10, 16, 20)
                   if s <= d.cin // 64]
+    if skinny_eligible(d):
+        # skinny variants (an ineligible variant reports an error or falls back; both are timed like the rest)
+        taps = d.kh * d.kw
+        cands += [(a, s) for a in range(SKINNY_FIRST, nalg + 1) for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20)
+                  if s <= d.cin // 64 and SKINNY_TAPS[a - SKINNY_FIRST] == taps]
     if getattr(ctx, "tune_only", None):   # tools/tune_gemm.py --try: the committed choice against these algos only
         cur = ctx.tune_only[1].get(conv_key(d))
         cands = ([cur] if cur else []) + [c for c in cands if c[0] in ctx.tune_only[0]]

@@ -536,7 +536,7 @@ def test_conv_halo_algos(ctx, algo, nsplit):
     ReLU-backward mask) vs torch fp32 on the bf16 values; bitwise reproducible run to run."""
     from depth_completion_amd import ops
     from depth_completion_amd.weights import pack_conv
-    assert _lib_num_algos() == 42
+    assert _lib_num_algos() == SKINNY_LAST
     cases = [  # n, c1, c2, cout, h, w, mode, epilogue
         (2, 128, 64, 96, 9, 35, 0, True), (1, 64, 0, 64, 18, 24, 1, False), (1, 320, 0, 320, 9, 12, 0, True),
         (1, 64, 0, 32, 13, 70, 0, False)]
@@ -570,6 +570,55 @@ def test_conv_halo_algos(ctx, algo, nsplit):
         ctx.step.zero_()
         assert rel(nchw(outs[0], n, h, w), ref) < 1e-2, (algo, nsplit, n, cin, cout, h, w, mode)
         assert torch.equal(outs[0], outs[1]), (algo, nsplit, n, cin, cout, h, w, mode)
+
+
+SKINNY_FIRST, SKINNY_LAST = 43, 54   # dc_conv_gemm algo ids of the weight-streaming skinny variants (conv_skinny.h)
+SKINNY_ALGOS = list(range(SKINNY_FIRST, SKINNY_LAST + 1))
+
+
+@pytest.mark.parametrize("algo", SKINNY_ALGOS)
+@pytest.mark.parametrize("nsplit", [1, 2, 3])
+def test_conv_skinny_algos(ctx, algo, nsplit):
+    """weight-streaming skinny conv / linear, every variant (3x3 halo tiles and 1x1 row tiles), input chunks split
+    over blocks: 3x3 direct / nearest-upsample / two-source concat, batch 2 with frames not a multiple of the tile,
+    output channels not a multiple of the block's 64 / 128, linears over rows not a multiple of the row tile, and
+    the full epilogue (bias, per-step row bias, residual, ReLU, ReLU-backward mask) vs torch fp32 on the bf16 values;
+    a variant given a shape outside its contract runs the im2col heuristic; bitwise reproducible run to run."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    cases = [  # n, c1, c2, cout, h, w, k, mode, epilogue
+        (1, 256, 0, 192, 9, 12, 3, 0, True), (2, 128, 128, 96, 7, 13, 3, 0, False), (1, 128, 0, 320, 18, 24, 3, 1, True),
+        (1, 512, 0, 200, 1, 300, 1, 0, True), (2, 256, 256, 128, 9, 12, 1, 0, False), (1, 128, 0, 64, 5, 7, 3, 0, False)]
+    for n, c1, c2, cout, h, w, k, mode, epi in cases:
+        cin = c1 + c2
+        hin, win = (h // 2, w // 2) if mode == 1 else (h, w)
+        xa = rnd(n, c1, hin, win, seed=90)
+        xb = rnd(n, c2, hin, win, seed=91) if c2 else None
+        wt = rnd(cout, cin, k, k, scale=1 / math.sqrt(cin * k * k), seed=92)
+        xin = torch.cat([xa, xb], 1) if c2 else xa
+        if mode == 1:
+            xin = F.interpolate(xin, size=(h, w), mode="nearest")
+        ref = F.conv2d(xin, wt, padding=k // 2)
+        kw = {}
+        if epi:
+            b = rnd(cout, seed=93)
+            table = rnd(4, cout, seed=94)
+            res = rnd(n, cout, h, w, seed=95)
+            mask = rnd(n, cout, h, w, seed=96)
+            ctx.step.fill_(1)
+            ref = torch.relu(ref + b.view(1, -1, 1, 1) + table[1].view(1, -1, 1, 1) + res) * (mask > 0)
+            kw = dict(bias=b, rowbias=table.to(torch.bfloat16), rowbias_ld=cout, resid=nhwc(res), act=1, mask=nhwc(mask))
+        outs = []
+        for _ in range(2):
+            y = torch.full((n * h * w, cout), 3.0, dtype=torch.bfloat16, device=dev)
+            ops.conv_gemm(ctx, nhwc(xa), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=hin, win=win, cin=cin,
+                          hout=h, wout=w, cout=cout, kh=k, kw=k, pad=k // 2, mode=mode, x2=nhwc(xb) if c2 else None,
+                          c1=c1 if c2 else 0, y=y, algo=algo, nsplit=nsplit, **kw)
+            torch.cuda.synchronize()
+            outs.append(y)
+        ctx.step.zero_()
+        assert rel(nchw(outs[0], n, h, w), ref) < 1e-2, (algo, nsplit, n, cin, cout, h, w, k, mode)
+        assert torch.equal(outs[0], outs[1]), (algo, nsplit, n, cin, cout, h, w, k, mode)
 
 
 def test_conv_halo_outside_contract_falls_back(ctx):

@@ -62,12 +62,12 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace3" -o run --output-format csv -- \
         python3 bench.py --batch 8 --steps 1 --warmup 1 --no-cpu-baseline > "$out/trace3_bench.json" 2> "$out/trace3.err" ;;
     pmc|pmc8)
-      # FETCH_SIZE, WRITE_SIZE and the MFMA-busy pass over the conv kernels (im2col and halo), eager step, 4 denoise
+      # FETCH_SIZE, WRITE_SIZE and the MFMA-busy pass over the conv kernels (im2col, halo and skinny), eager step, 4 denoise
       # steps; each pass its own run (rocprofv3 does not split counters over passes)
       b=1; [ "$step" = pmc8 ] && b=8
       for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE:mfma"; do
         # shellcheck disable=SC2086
-        timeout -s KILL 180 rocprofv3 --pmc ${pass%%:*} --kernel-include-regex "conv_(gemm|halo)_kernel" \
+        timeout -s KILL 180 rocprofv3 --pmc ${pass%%:*} --kernel-include-regex "conv_(gemm|halo|skinny)_kernel" \
           -d "$out/pmc${b}_${pass##*:}" -o run --output-format csv -- python3 bench.py --no-graph --steps 1 --warmup 0 \
           --no-cpu-baseline --denoise-steps 4 --batch $b > "$out/pmc${b}_${pass##*:}.json" 2> "$out/pmc${b}_${pass##*:}.err"
       done ;;

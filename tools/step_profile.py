@@ -4,7 +4,7 @@ Run:   rocprofv3 --kernel-trace -d <dir> -o run --output-format csv -- python3 t
        python tools/step_profile.py --trace <dir>/run_kernel_trace.csv --descs <descs.json>
 The first form runs a C2 call (graph-replayed guided steps) and writes the conv launches of one step, in launch
 order, with their shapes and chosen variants.  The second (CPU) takes the last complete step of the trace, matches
-its conv dispatches (conv_gemm_kernel / conv_halo_kernel) to those launches by order, and prints the time per shape
+its conv dispatches (conv_gemm_kernel / conv_halo_kernel / conv_skinny_kernel) to those launches by order, and prints the time per shape
 group -- the step's own cache state and launch order, unlike tools/conv_breakdown.py's warm replays.
 """
 import argparse
@@ -67,7 +67,7 @@ def analyse(trace, descs_path):
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    conv = [r for r in rows if "conv_gemm_kernel" in r[2] or "conv_halo_kernel" in r[2]]
+    conv = [r for r in rows if any(k in r[2] for k in ("conv_gemm_kernel", "conv_halo_kernel", "conv_skinny_kernel"))]
     n = len(descs)
     last = conv[-n:]   # the final step of the last call is the last n conv dispatches (final decode is dense:
     # skip back over the final decode's convs by aligning on shapes below)
@@ -75,7 +75,8 @@ def analyse(trace, descs_path):
     best = None
     for off in range(0, min(len(conv) - n, 200) + 1):
         win = conv[len(conv) - n - off:len(conv) - off]
-        ok = sum(("halo" in w[2]) == (d["algo"] >= 23) for w, d in zip(win, descs))
+        fam = lambda a: "halo" if 23 <= a <= 36 else ("skinny" if a >= 43 else "gemm")   # noqa: E731
+        ok = sum((fam(d["algo"]) in w[2]) or (fam(d["algo"]) == "skinny") for w, d in zip(win, descs))
         if best is None or ok > best[0]:
             best = (ok, win)
         if ok == n:
