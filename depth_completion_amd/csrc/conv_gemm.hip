@@ -58,7 +58,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
-  if (d->algo < 0 || d->algo > kNumAll + kNumSkinny || d->splitk < -4) return DC_ERR_ARG;
+  if (d->algo < 0 || d->algo > kNumAll + kNumSkinny || d->splitk < (d->algo > kNumAll ? -32 : -4)) return DC_ERR_ARG;
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;
@@ -121,8 +121,8 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (algo > kNumAll) {
     const int si = algo - kNumAll - 1;
     if (skinny_eligible(p, si))
-      return kSkinnyAlgos[si].kt == 9 ? conv_launch_skinny9(si, p, splits <= 0 ? 1 : splits, s)
-                                      : conv_launch_skinny1(si, p, splits <= 0 ? 1 : splits, s);
+      return kSkinnyAlgos[si].kt == 9 ? conv_launch_skinny9(si, p, splits == 0 ? 1 : splits, s)
+                                      : conv_launch_skinny1(si, p, splits == 0 ? 1 : splits, s);
     algo = 0;   // a skinny choice carried to a shape outside its contract (nearest-shape pick): im2col heuristic
     splits = 0;
   }

@@ -19,8 +19,9 @@
 //     rows) go into LDS by LDS-DMA one group ahead (double-buffered), with one barrier per group; all four waves
 //     read them as the A fragments (ds_read_b128, conflict-free swizzle, per-lane addresses precomputed for the
 //     three kx phases, the second k-step one XOR away).
-// Input chunks split over blocks (split-K) are summed in split order by the tile's last-arriving block
-// (tile_handoff_g, deterministic); the epilogue stages the tile block-wide in LDS and writes 16-B rows.
+// Input chunks split over blocks (split-K) are summed in split order, deterministically, either by the tile's
+// last-arriving block (splitk > 0) or by a second kernel over (tile, fragment row) (splitk < 0); the epilogue stages
+// the tile in LDS and writes 16-B rows.
 // Contract (skinny_eligible): KT 9 = the halo contract (3x3, stride 1, pad 1, direct or nearest-upsample input,
 // whole 64-channel chunks); KT 1 = 1x1 / linear over whole 64-channel chunks; no row list, no GEGLU, no fused
 // GroupNorm statistics; input chunks a multiple of U.
@@ -259,8 +260,26 @@ struct SkinnyBlock {
     }
     vm_wait<0>();
 
-    if (p.splits > 1 && !handoff(lb, split, tiles)) return;
+    if (p.splits > 1) {
+      if (p.sk_blocks < 0) {   // two-kernel form: the partial only; skinny_reduce_kernel sums and stores
+        store_partial(lb, split, tiles);
+        return;
+      }
+      if (!handoff(lb, split, tiles)) return;
+    }
     epilogue(wid, M);
+  }
+
+  // ---- two-kernel split-K: this split's partial in the accumulator-native slab layout (the kernel boundary orders
+  // it before skinny_reduce_kernel's reads)
+  __device__ __forceinline__ void store_partial(int lb, int split, int tiles) {
+    constexpr int FR = MI * NJ, WAVE_F = FR * 256, TILE_F = 4 * WAVE_F;
+    const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
+    const long mine = ((long)split * tiles + lb) * TILE_F + (threadIdx.x >> 6) * WAVE_F + lane * 4;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) store_sc1_x4(rs, mine + (i * NJ + j) * 256, acc[i][j]);
   }
 
   // ---- split-K hand-off (the protocol of tile_handoff_g: sc1 partial stores, agent-scope arrival counter, the
@@ -360,6 +379,60 @@ __global__ __launch_bounds__(256) void conv_skinny_kernel(const ConvGemmParams p
   blk.run();
 }
 
+// Two-kernel split-K (splitk < 0): the last-arriving block of a skinny tile would read every split's partial alone
+// (splits x BMP x BN x 4 bytes through one CU, latency- and per-CU-bandwidth-bound); here one block per (tile, 16-pixel
+// fragment row) sums that row's partials in split order (deterministic), adds the bias and runs the epilogue.
+template <int KT, int TH, int TW, int NJ, int U>
+__global__ __launch_bounds__(256) void skinny_reduce_kernel(const ConvGemmParams p) {
+  using C = SkinnyCfg<KT, TH, TW, NJ, U>;
+  constexpr int FR = C::MI * NJ, WAVE_F = FR * 256, TILE_F = 4 * WAVE_F;
+  __shared__ __attribute__((aligned(16))) bf16 es[16 * C::LDE];
+  const int lb = blockIdx.x, ii = blockIdx.y, tiles = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tiles_n = (p.cout + C::BN - 1) / C::BN, tiles_sp = tiles / tiles_n;
+  const int tn = lb / tiles_sp, sp = lb - tn * tiles_sp;
+  const int n0 = tn * C::BN;
+  const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
+  const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) {
+    const long off = (long)lb * TILE_F + wid * WAVE_F + (ii * NJ + jj) * 256 + lane * 4;
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int k = 0; k < p.splits; ++k) s += load_sc1_x4(rs, off + (long)k * tiles * TILE_F);
+    const int cl = wid * C::WN + jj * 16 + col_l;
+    const int c = n0 + cl;
+    const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) es[(row_l + e) * C::LDE + cl] = (bf16)(s[e] + bv);
+  }
+  __syncthreads();
+  if (p.diag & 64) return;
+  constexpr int GPR = C::BN / 8;
+  const long M = conv_rows(p);
+  for (int g = tid; g < 16 * GPR; g += 256) {
+    const int r = g / GPR, cg = g - (g / GPR) * GPR;
+    const int pl = ii * 16 + r;
+    const int c = n0 + cg * 8;
+    if (pl >= C::BM || c >= p.cout) continue;
+    long m;
+    if constexpr (KT == 9) {
+      const int tiles_x = (p.wout + TW - 1) / TW, tiles_y = (p.hout + TH - 1) / TH;
+      const int frame = sp / (tiles_y * tiles_x);
+      const int trem = sp - frame * (tiles_y * tiles_x);
+      const int oy = (trem / tiles_x) * TH + pl / TW, ox = (trem - (trem / tiles_x) * tiles_x) * TW + pl % TW;
+      if (oy >= p.hout || ox >= p.wout) continue;
+      m = ((long)frame * p.hout + oy) * p.wout + ox;
+    } else {
+      m = (long)sp * TH + pl;
+      if (m >= M) continue;
+    }
+    float v[8];
+    load8(es + r * C::LDE + cg * 8, v);
+    epilogue_store(p, m, c, v, false);
+  }
+}
+
 // skinny variants: taps (9: halo tile TH x TW of one frame; 1: TH token / pixel rows), NJ x 64 output channels per
 // block, U input chunks per group
 struct SkinnyAlgo {
@@ -404,16 +477,21 @@ int launch_skinny(ConvGemmParams& p, int splits, hipStream_t stream) {
   const int tiles = (int)tiles_l;
   const int ngr = (p.cin / 64) / U;
   p.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(p.ws) + (p.ws_bytes - kCounterBytes));
-  splits = max(1, min(splits, ngr));   // stream-K requests (< 0) run unsplit
+  const bool sep = splits < 0;          // two-kernel split-K (skinny_reduce_kernel)
+  splits = max(1, min(sep ? -splits : splits, ngr));
   if (p.ws == nullptr || tiles > kMaxSplitTiles) splits = 1;
   while (splits > 1 && (long)splits * tiles * Cf::BMP * Cf::BN * 4 > p.ws_bytes - kCounterBytes) --splits;
   const int gps = (ngr + splits - 1) / splits;   // groups per split
   splits = (ngr + gps - 1) / gps;
   p.kps = gps * U;
   p.splits = splits;
-  p.sk_blocks = 0;
+  p.sk_blocks = (sep && splits > 1) ? -1 : 0;
   hipLaunchKernelGGL((conv_skinny_kernel<KT, TH, TW, NJ, U>), dim3(tiles, splits), dim3(256), 0, stream, p);
   DC_CHECK_LAUNCH();
+  if (p.sk_blocks < 0) {
+    hipLaunchKernelGGL((skinny_reduce_kernel<KT, TH, TW, NJ, U>), dim3(tiles, Cf::MI), dim3(256), 0, stream, p);
+    DC_CHECK_LAUNCH();
+  }
   return DC_OK;
 }
 

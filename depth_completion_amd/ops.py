@@ -242,8 +242,10 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     if skinny_eligible(d):
         # skinny variants (an ineligible variant reports an error or falls back; both are timed like the rest)
         taps = d.kh * d.kw
-        cands += [(a, s) for a in range(SKINNY_FIRST, nalg + 1) for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20)
-                  if s <= d.cin // 64 and SKINNY_TAPS[a - SKINNY_FIRST] == taps]
+        # (splitk < 0: the same split with the partials summed by a second kernel instead of the last-arriving block)
+        cands += [(a, s) for a in range(SKINNY_FIRST, nalg + 1)
+                  for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, -2, -4, -6, -8, -10, -12, -16, -20)
+                  if abs(s) <= d.cin // 64 and SKINNY_TAPS[a - SKINNY_FIRST] == taps]
     if getattr(ctx, "tune_only", None):   # tools/tune_gemm.py --try: the committed choice against these algos only
         cur = ctx.tune_only[1].get(conv_key(d))
         cands = ([cur] if cur else []) + [c for c in cands if c[0] in ctx.tune_only[0]]

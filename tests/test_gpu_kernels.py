@@ -577,10 +577,11 @@ SKINNY_ALGOS = list(range(SKINNY_FIRST, SKINNY_LAST + 1))
 
 
 @pytest.mark.parametrize("algo", SKINNY_ALGOS)
-@pytest.mark.parametrize("nsplit", [1, 2, 3])
+@pytest.mark.parametrize("nsplit", [1, 2, 3, -2, -5])
 def test_conv_skinny_algos(ctx, algo, nsplit):
     """weight-streaming skinny conv / linear, every variant (3x3 halo tiles and 1x1 row tiles), input chunks split
-    over blocks: 3x3 direct / nearest-upsample / two-source concat, batch 2 with frames not a multiple of the tile,
+    over blocks (nsplit > 0: summed by the last-arriving block; < 0: by the second, reduce kernel): 3x3 direct /
+    nearest-upsample / two-source concat, batch 2 with frames not a multiple of the tile,
     output channels not a multiple of the block's 64 / 128, linears over rows not a multiple of the row tile, and
     the full epilogue (bias, per-step row bias, residual, ReLU, ReLU-backward mask) vs torch fp32 on the bf16 values;
     a variant given a shape outside its contract runs the im2col heuristic; bitwise reproducible run to run."""

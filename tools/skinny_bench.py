@@ -98,11 +98,11 @@ def main():
         ref = y.float().clone()
         flops = 2.0 * nb * hout * wout * cout * ktot
         name = f"{'lin' if kk == 1 else 'c3'} M={nb * hout * wout} N={cout} K={ktot}" + (" up" if mode == 1 else "")
-        print(f"{name:32s} tuned {tuned}: {t0:7.1f} us  {flops / t0 / 1e6:6.1f} TF/s  {wbytes / t0 / 1e3:6.2f} TB/s",
+        print(f"{name:32s} tuned {tuned}: {t0:7.1f} us  {flops / t0 / 1e6:6.1f} TF/s  {wbytes / t0 / 1e3:7.1f} GB/s",
               flush=True)
         best = (t0, tuned)
         for a in algos:
-            for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20):
+            for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, -4, -6, -8, -10, -12, -16, -20):
                 try:
                     ds = descs(a, s)
                     y.zero_()
@@ -115,7 +115,7 @@ def main():
                 flag = " *" if t < best[0] else ""
                 if t < best[0]:
                     best = (t, (a, s))
-                print(f"    ({a:2d},{s:2d}) {t:7.1f} us  {flops / t / 1e6:6.1f} TF/s  {wbytes / t / 1e3:6.2f} TB/s  "
+                print(f"    ({a:2d},{s:2d}) {t:7.1f} us  {flops / t / 1e6:6.1f} TF/s  {wbytes / t / 1e3:7.1f} GB/s  "
                       f"err {err:.1e}{flag}", flush=True)
         print(f"  best {best[1]} {best[0]:.1f} us ({t0 / best[0]:.2f}x)", flush=True)
 
