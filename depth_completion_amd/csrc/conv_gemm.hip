@@ -7,9 +7,12 @@ namespace {
 }  // namespace
 int conv_launch_skinny9(int i, ConvGemmParams& p, int splits, hipStream_t s);
 int conv_launch_skinny1(int i, ConvGemmParams& p, int splits, hipStream_t s);
+int conv_launch_resident(int i, ConvGemmParams& p, int bpc, hipStream_t s);
 
-// external algo ids: 1 .. kNumAll im2col / halo variants (conv_gemm_impl.h), then the weight-streaming skinny variants
-extern "C" int dc_conv_num_algos(void) { return kNumAll + kNumSkinny; }
+// external algo ids: 1 .. kNumAll im2col / halo variants (conv_gemm_impl.h), then the weight-streaming skinny variants,
+// then the weight-resident persistent narrow convs (conv_skinny.h)
+constexpr int kNumExt = kNumAll + kNumSkinny + kNumResident;
+extern "C" int dc_conv_num_algos(void) { return kNumExt; }
 
 extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (!d || !d->x || !d->w || !d->y) return DC_ERR_ARG;
@@ -58,7 +61,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
-  if (d->algo < 0 || d->algo > kNumAll + kNumSkinny || d->splitk < (d->algo > kNumAll ? -32 : -4)) return DC_ERR_ARG;
+  if (d->algo < 0 || d->algo > kNumExt || d->splitk < (d->algo > kNumAll ? -32 : -4)) return DC_ERR_ARG;
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;
@@ -118,6 +121,12 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
+  if (algo > kNumAll + kNumSkinny) {
+    const int ri = algo - kNumAll - kNumSkinny - 1;
+    if (resident_eligible(p)) return conv_launch_resident(ri, p, splits, s);
+    algo = 0;   // outside the narrow-conv contract (nearest-shape pick): im2col heuristic
+    splits = 0;
+  }
   if (algo > kNumAll) {
     const int si = algo - kNumAll - 1;
     if (skinny_eligible(p, si))

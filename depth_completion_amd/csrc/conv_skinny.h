@@ -511,3 +511,246 @@ int launch_skinny_idx(int i, ConvGemmParams& p, int splits, hipStream_t s) {
     default: return DC_ERR_ARG;
   }
 }
+
+// ---------------------------------------------------------------------------------------------------------
+// Weight-resident persistent 3x3 conv for the narrow layers (cin = 64, cout <= 64: the TAESD encoder / decoder convs
+// and their input gradients, every guided step at up to 288 x 384).  A 64 x 576 weight is 72 KB: each wave keeps its
+// 16 output channels' 18 B fragments in VGPRs for the whole launch, and a block walks tiles t = blockIdx.x, +gridDim.x
+// with the (TH+2) x (TW+2) halo of the next tile in flight (LDS-DMA into the other of two slots) while the current tile
+// runs its 9 taps; the epilogue stages the tile in its own LDS region.  Per tile that leaves one barrier and the
+// previous tile's stores left in flight (a static store count per tile, so the tile head waits only for its halo).  The halo-tile kernel (conv_halo_kernel) pays the weight ring's fill and its drain per tile.
+template <int TH, int TW>
+struct ResidentBlock {
+  using C = SkinnyCfg<9, TH, TW, 1, 1>;   // halo geometry; 64 output channels (16 per wave); one 64-channel chunk
+  static constexpr int MI = C::MI, G = C::G, LA = C::LA;
+  static constexpr int L = G * MI;
+  static constexpr int D = 8 < L ? 8 : L;
+  static constexpr int ES = C::RING;                 // epilogue staging after the two halo slots
+  static constexpr int LDS = C::RING + C::EPI;
+  static constexpr int kOOB = (int)0x80000000u;
+  static_assert(C::SLOT + 2 * C::W8 * 128 + 2 * 128 < 65536, "slot and tap offsets as ds_read immediates");
+  static_assert(LDS <= 160 * 1024, "LDS");
+
+  const ConvGemmParams& p;
+  char* smem;
+  int lane, wid_s, tiles_x, tiles_y;
+  int ab[MI][3];
+  __amdgpu_buffer_rsrc_t ra, rb;
+  f32x4 acc[MI];
+  bf16x8 wr[G];
+
+  __device__ __forceinline__ void coords(int t, int& frame, int& oy0, int& ox0) const {
+    frame = t / (tiles_y * tiles_x);
+    const int r = t - frame * (tiles_y * tiles_x);
+    oy0 = (r / tiles_x) * TH;
+    ox0 = (r - (r / tiles_x) * tiles_x) * TW;
+  }
+  __device__ __forceinline__ void issue_halo(int t, int slot) {
+    int frame, oy0, ox0;
+    coords(t, frame, oy0, ox0);
+    const int tid = threadIdx.x, sl = tid & 7, r0 = tid >> 3;
+    DC_LDS char* b = (DC_LDS char*)smem + slot * C::SLOT;
+#pragma unroll
+    for (int j = 0; j < LA; ++j) {
+      const int hr = r0 + 32 * j;
+      const int hy = hr / C::W8, hx = hr - (hr / C::W8) * C::W8;
+      const int vy = oy0 - 1 + hy, vx = ox0 - 1 + hx;
+      const bool ok = hr < C::AROWS && hx < TW + 2 && vy >= 0 && vy < p.hout && vx >= 0 && vx < p.wout;
+      int iy = vy, ix = vx;
+      if (p.mode == 1) {
+        iy = ok ? (int)fast_div((unsigned)(vy * p.hin), p.h_mul, p.h_shr) : 0;
+        ix = ok ? (int)fast_div((unsigned)(vx * p.win), p.w_mul, p.w_shr) : 0;
+      }
+      const long pix = ((long)frame * p.hin + iy) * p.win + ix;
+      const int off = ok ? (int)((pix * p.ldx + (sl ^ (hr & 7)) * 8) * 2) : kOOB;
+      buf_load_lds16(ra, b + (wid_s * 64 + 256 * j) * 16, off, 0);
+    }
+  }
+  template <int PAR, int F>
+  __device__ __forceinline__ void read_frag(bf16x8 (&af)[D]) {
+    constexpr int S = F / MI, II = F % MI;
+    constexpr int T = S / 2, H = S % 2, KY = T / 3, KX = T % 3;
+    constexpr int IMM = PAR * C::SLOT + KY * C::W8 * 128;
+    const int a = H ? (ab[II][KX] ^ 64) : ab[II][KX];
+    af[F % D] = *reinterpret_cast<const bf16x8*>(smem + a + IMM);
+  }
+  template <int PAR, int F>
+  __device__ __forceinline__ void frag_step(bf16x8 (&af)[D]) {
+    constexpr int S = F / MI, II = F % MI;
+    acc[II] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[F % D], wr[S], acc[II], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if constexpr (F + D < L) {
+      read_frag<PAR, F + D>(af);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  }
+  template <int PAR, int... P>
+  __device__ __forceinline__ void read_first(bf16x8 (&af)[D], std::integer_sequence<int, P...>) {
+    (read_frag<PAR, P>(af), ...);
+  }
+  template <int PAR, int... F>
+  __device__ __forceinline__ void compute(std::integer_sequence<int, F...>) {
+    bf16x8 af[D];
+    read_first<PAR>(af, std::make_integer_sequence<int, D>{});
+    __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+    (frag_step<PAR, F>(af), ...);
+  }
+
+  // one tile: its halo (slot PAR) has landed after the wait; the next tile's goes into the other slot
+  template <int PAR>
+  __device__ __forceinline__ void tile(int t, int tnext, int tiles) {
+    vm_wait<NIT>();   // this tile's halo; the previous tile's NIT stores (younger) may still be in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (tnext < tiles) issue_halo(tnext, PAR ^ 1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    compute<PAR>(std::make_integer_sequence<int, L>{});
+    epilogue(t);
+  }
+
+  // Exactly NIT 16-B stores per thread per tile (pixels outside the frame store out of range: dropped), so that the
+  // next tile's head waits for its halo with a static vmcnt(NIT) and leaves this tile's stores in flight.
+  static constexpr int NIT = C::BM * (C::BN / 8) / 256;
+  static_assert(C::BM * (C::BN / 8) % 256 == 0, "whole store rounds");
+  __device__ __forceinline__ void epilogue(int t) {
+    int frame, oy0, ox0;
+    coords(t, frame, oy0, ox0);
+    const int wid = threadIdx.x >> 6;
+    const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+    bf16* es = reinterpret_cast<bf16*>(smem + ES);
+    const int cl = wid * 16 + col_l;
+    const float bv = (p.bias && cl < p.cout) ? p.bias[cl] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) es[(i * 16 + row_l + q) * C::LDE + cl] = (bf16)(acc[i][q] + bv);
+    __syncthreads();
+    constexpr int GPR = C::BN / 8;
+    const __amdgpu_buffer_rsrc_t ry = buf_rsrc(p.y);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int g = threadIdx.x + 256 * it;
+      const int pl = g / GPR, cg = g - (g / GPR) * GPR;
+      const int c = cg * 8;
+      const int oy = oy0 + pl / TW, ox = ox0 + (pl - (pl / TW) * TW);
+      const bool ok = c < p.cout && oy < p.hout && ox < p.wout && !(p.diag & 64);
+      const long m = ok ? ((long)frame * p.hout + oy) * p.wout + ox : 0;
+      float v[8];
+      load8(es + pl * C::LDE + c, v);
+      if (p.rowbias) {
+        const bf16* rb = p.rowbias + (long)(*p.rowbias_idx) * p.rowbias_ld + c;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (float)(bf16)v[i] + (ok ? (float)rb[i] : 0.0f);
+      }
+      if (p.resid && ok) {
+        float rf[8];
+        load8(p.resid + m * p.ldr + c, rf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = (float)(bf16)v[i] + rf[i];
+      }
+      if (p.act == 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = fmaxf(v[i], 0.0f);
+      }
+      if (p.mask && ok) {
+        float mf[8];
+        load8(p.mask + m * p.ldmask + c, mf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = mf[i] > 0.0f ? v[i] : 0.0f;
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, o), ry, ok ? (int)((m * p.ldy + c) * 2) : kOOB,
+                                             0, 0);
+    }
+  }
+
+  __device__ __forceinline__ void run() {
+    const int tid = threadIdx.x;
+    lane = tid & 63;
+    wid_s = __builtin_amdgcn_readfirstlane(tid >> 6);
+    tiles_x = (p.wout + TW - 1) / TW;
+    tiles_y = (p.hout + TH - 1) / TH;
+    const int tiles = p.nb * tiles_x * tiles_y;
+    int t = blockIdx.x;
+    const int step = gridDim.x;
+    if (t >= tiles) return;
+    ra = buf_rsrc(p.x);
+    rb = buf_rsrc(p.w);
+    // the wave's 16 output channels x 576 weights, once: B fragments of the 18 k-steps (tap T, half H)
+    const int co = (tid >> 6) * 16 + (lane & 15);
+    const int wo = co < p.cout ? (co * p.ktot + 8 * (lane >> 4)) * 2 : kOOB;
+#pragma unroll
+    for (int s = 0; s < G; ++s)
+      wr[s] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, wo, ((s / 2) * 64 + (s % 2) * 32) * 2, 0));
+#pragma unroll
+    for (int ii = 0; ii < MI; ++ii) {
+      int pl = ii * 16 + (lane & 15);
+      pl = pl < C::BM ? pl : 0;
+      const int rbase = (pl / TW) * C::W8 + (pl - (pl / TW) * TW);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int r = rbase + kx;
+        ab[ii][kx] = r * 128 + (((lane >> 4) ^ (r & 7)) << 4);
+      }
+    }
+    issue_halo(t, 0);
+    vm_wait<0>();   // the weights and the first halo
+    for (;;) {
+      tile<0>(t, t + step, tiles);
+      t += step;
+      if (t >= tiles) break;
+      tile<1>(t, t + step, tiles);
+      t += step;
+      if (t >= tiles) break;
+    }
+    vm_wait<0>();
+  }
+};
+
+template <int TH, int TW>
+__global__ __launch_bounds__(256) void conv_resident_kernel(const ConvGemmParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[ResidentBlock<TH, TW>::LDS];
+  ResidentBlock<TH, TW> blk{p, smem};
+  blk.run();
+}
+
+// resident variants (TH, TW): 8 x 16 (78 KB LDS, two blocks per CU), 8 x 32 (138 KB, one), 4 x 32 (78 KB), 4 x 16 (49 KB)
+struct ResidentAlgo {
+  int th, tw;
+};
+constexpr ResidentAlgo kResidentAlgos[] = {{8, 16}, {8, 32}, {4, 32}, {4, 16}};
+constexpr int kNumResident = sizeof(kResidentAlgos) / sizeof(kResidentAlgos[0]);
+
+bool resident_eligible(const ConvGemmParams& p) {
+  return p.gn.mode == 0 && p.cin == 64 && p.cout <= 64 && p.cout % 8 == 0 && p.c1 >= p.cin && halo_eligible(p) &&
+         (long)p.nb * p.hout * p.wout * p.ldy * 2 < (1L << 31);
+}
+
+// bpc: blocks per CU of the persistent grid (the dc_conv_desc split field; 0: as many as the LDS allows)
+template <int TH, int TW>
+int launch_resident(ConvGemmParams& p, int bpc, hipStream_t stream) {
+  const long tiles_l = (long)p.nb * ((p.hout + TH - 1) / TH) * ((p.wout + TW - 1) / TW);
+  if (tiles_l >= (1L << 30)) return DC_ERR_ARG;
+  const int fit = (int)((160L * 1024) / ResidentBlock<TH, TW>::LDS);
+  bpc = bpc <= 0 ? fit : min(bpc, fit);
+  const int grid = (int)min(tiles_l, (long)bpc * 256);
+  p.splits = 1;
+  p.sk_blocks = 0;
+  hipLaunchKernelGGL((conv_resident_kernel<TH, TW>), dim3(grid), dim3(256), 0, stream, p);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+
+int launch_resident_idx(int i, ConvGemmParams& p, int bpc, hipStream_t s) {
+  switch (i) {
+#define DC_RESIDENT(i) \
+  case i: return launch_resident<kResidentAlgos[i].th, kResidentAlgos[i].tw>(p, bpc, s);
+    DC_RESIDENT(0) DC_RESIDENT(1) DC_RESIDENT(2) DC_RESIDENT(3)
+#undef DC_RESIDENT
+    default: return DC_ERR_ARG;
+  }
+}

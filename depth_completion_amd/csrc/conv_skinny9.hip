@@ -9,3 +9,5 @@ namespace {
 int conv_launch_skinny9(int i, ConvGemmParams& p, int splits, hipStream_t s) {
   return launch_skinny_idx<9>(i, p, splits, s);
 }
+
+int conv_launch_resident(int i, ConvGemmParams& p, int bpc, hipStream_t s) { return launch_resident_idx(i, p, bpc, s); }

@@ -190,7 +190,8 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
 HALO_FIRST, HALO_LAST = 23, 36   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv (conv_gemm_impl.h); ids
 # 1 .. 22 and 37 .. 42 are im2col tile variants, SKINNY_FIRST .. dc_conv_num_algos() the weight-streaming skinny
 # conv / linear variants (conv_skinny.h)
-IM2COL_LAST, SKINNY_FIRST = 42, 43
+IM2COL_LAST, SKINNY_FIRST, RESIDENT_FIRST = 42, 43, 55   # RESIDENT_FIRST ..: the weight-resident persistent
+# narrow convs (cin 64, cout <= 64; their split field is the persistent grid's blocks per CU)
 SKINNY_TAPS = (9, 9, 9, 9, 9, 1, 1, 1, 1, 1, 1, 1)   # taps of skinny variant SKINNY_FIRST + i (conv_skinny.h kSkinnyAlgos)
 
 
@@ -243,12 +244,14 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
         # skinny variants (an ineligible variant reports an error or falls back; both are timed like the rest)
         taps = d.kh * d.kw
         # (splitk < 0: the same split with the partials summed by a second kernel instead of the last-arriving block)
-        cands += [(a, s) for a in range(SKINNY_FIRST, nalg + 1)
+        cands += [(a, s) for a in range(SKINNY_FIRST, RESIDENT_FIRST)
                   for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, -2, -4, -6, -8, -10, -12, -16, -20)
                   if abs(s) <= d.cin // 64 and SKINNY_TAPS[a - SKINNY_FIRST] == taps]
     if getattr(ctx, "tune_only", None):   # tools/tune_gemm.py --try: the committed choice against these algos only
         cur = ctx.tune_only[1].get(conv_key(d))
         cands = ([cur] if cur else []) + [c for c in cands if c[0] in ctx.tune_only[0]]
+    if halo_eligible(d) and d.cin == 64 and d.cout <= 64 and not d.gn and not d.x2:
+        cands += [(a, b) for a in range(RESIDENT_FIRST, nalg + 1) for b in (0, 1, 2, 3)]
     best, best_t = (0, 0), float("inf")
     # DC_TUNE_COLD=1: every timed call starts with L2 and the Infinity Cache flushed (a 512 MiB write),
     # as the weights are in the sampler step (each is touched once per pass)

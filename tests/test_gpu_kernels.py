@@ -536,7 +536,7 @@ def test_conv_halo_algos(ctx, algo, nsplit):
     ReLU-backward mask) vs torch fp32 on the bf16 values; bitwise reproducible run to run."""
     from depth_completion_amd import ops
     from depth_completion_amd.weights import pack_conv
-    assert _lib_num_algos() == SKINNY_LAST
+    assert _lib_num_algos() == RESIDENT_LAST
     cases = [  # n, c1, c2, cout, h, w, mode, epilogue
         (2, 128, 64, 96, 9, 35, 0, True), (1, 64, 0, 64, 18, 24, 1, False), (1, 320, 0, 320, 9, 12, 0, True),
         (1, 64, 0, 32, 13, 70, 0, False)]
@@ -574,6 +574,45 @@ def test_conv_halo_algos(ctx, algo, nsplit):
 
 SKINNY_FIRST, SKINNY_LAST = 43, 54   # dc_conv_gemm algo ids of the weight-streaming skinny variants (conv_skinny.h)
 SKINNY_ALGOS = list(range(SKINNY_FIRST, SKINNY_LAST + 1))
+RESIDENT_FIRST, RESIDENT_LAST = 55, 58   # ... of the weight-resident persistent narrow convs (conv_skinny.h)
+
+
+@pytest.mark.parametrize("algo", list(range(RESIDENT_FIRST, RESIDENT_LAST + 1)))
+@pytest.mark.parametrize("bpc", [0, 1, 2])
+def test_conv_resident_algos(ctx, algo, bpc):
+    """weight-resident persistent 3x3 conv (cin 64, cout <= 64; bpc: blocks per CU of the persistent grid, 0 = as
+    many as fit): direct and nearest-upsample input, batch 2 with frames not a multiple of the tile, more tiles than
+    blocks (each block walks several, alternating halo slots), cout 64 / 48, the full epilogue (bias, residual,
+    ReLU, ReLU-backward mask) vs torch fp32 on the bf16 values; shapes outside the contract (cout 3, cin 128) run
+    the im2col heuristic; bitwise reproducible run to run."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import pack_conv
+    cases = [  # n, cin, cout, h, w, mode, epilogue
+        (1, 64, 64, 144, 192, 0, True), (2, 64, 48, 37, 70, 0, False), (1, 64, 64, 72, 96, 1, True),
+        (1, 64, 3, 40, 40, 0, False), (1, 128, 64, 18, 24, 0, False)]
+    for n, cin, cout, h, w, mode, epi in cases:
+        hin, win = (h // 2, w // 2) if mode == 1 else (h, w)
+        x = rnd(n, cin, hin, win, seed=100)
+        wt = rnd(cout, cin, 3, 3, scale=1 / math.sqrt(cin * 9), seed=101)
+        xin = F.interpolate(x, size=(h, w), mode="nearest") if mode == 1 else x
+        ref = F.conv2d(xin, wt, padding=1)
+        kw = {}
+        if epi:
+            b = rnd(cout, seed=102)
+            res = rnd(n, cout, h, w, seed=103)
+            mask = rnd(n, cout, h, w, seed=104)
+            ref = torch.relu(ref + b.view(1, -1, 1, 1) + res) * (mask > 0)
+            kw = dict(bias=b, resid=nhwc(res), act=1, mask=nhwc(mask))
+        outs = []
+        for _ in range(2):
+            ldy = -(-cout // 8) * 8
+            y = torch.full((n * h * w, ldy), 3.0, dtype=torch.bfloat16, device=dev)
+            ops.conv_gemm(ctx, nhwc(x), pack_conv(wt).to(dev, torch.bfloat16), nb=n, hin=hin, win=win, cin=cin,
+                          hout=h, wout=w, cout=cout, mode=mode, y=y, algo=algo, nsplit=bpc, **kw)
+            torch.cuda.synchronize()
+            outs.append(y[:, :cout])
+        assert rel(nchw(outs[0].contiguous(), n, h, w), ref) < 1e-2, (algo, bpc, n, cin, cout, h, w, mode)
+        assert torch.equal(outs[0], outs[1]), (algo, bpc, n, cin, cout, h, w, mode)
 
 
 @pytest.mark.parametrize("algo", SKINNY_ALGOS)

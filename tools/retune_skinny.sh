@@ -7,7 +7,7 @@ tag=${1:?tag}
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-DC_TUNE_COLD=2 timeout -k 10 900 python -u tools/tune_gemm.py --try $(seq 43 54) --workloads c2:1 c4:1 \
+DC_TUNE_COLD=2 timeout -k 10 900 python -u tools/tune_gemm.py --try ${IDS:-$(seq 43 54)} --workloads ${WL:-c2:1 c4:1} \
   --out $out/tuned.json > $out/tune.log 2>&1
 for i in 1 2; do
   timeout -k 10 300 python -u bench.py --no-cpu-baseline > $out/c2_old_$i.json 2> $out/c2_old_$i.err

@@ -5,7 +5,8 @@ Cache), so the weights stream from HBM as they do in the sampler step, where eac
 per pass.  For each shape: the committed table's (algo, split), then every skinny algo x split; the output's
 relative error against the tuned launch is a quick correctness screen (tests/test_gpu_kernels.py has the real tests).
 Reports us per launch, TF/s and the weight-stream rate (weight bytes / time).
-Usage: python tools/skinny_bench.py [--reps 20] [--set l2|l3|all] [--algos 43 44 ...]
+Usage: python tools/skinny_bench.py [--reps 20] [--set l2|l3|taesd|all] [--algos 43 44 ...]
+(taesd: the 64-channel decoder convs, for the weight-resident persistent variants, algo ids 55..)
 """
 import argparse
 import ctypes as C
@@ -26,6 +27,8 @@ L2 = [(1, 18, 24, 1280, 18, 24, 1280, 0), (1, 18, 24, 2560, 18, 24, 1280, 0), (1
       (1, 9, 12, 1280, 18, 24, 1280, 1), (1, 18, 24, 640, 18, 24, 1280, 0), (1, 18, 24, 1280, 18, 24, 640, 0),
       ("lin", 432, 1280, 1280), ("lin", 432, 10240, 1280), ("lin", 432, 5120, 1280), ("lin", 432, 1280, 3840),
       ("lin", 432, 3840, 1280), ("lin", 432, 2560, 1280)]
+TAESD = [(1, 288, 384, 64, 288, 384, 64, 0), (1, 144, 192, 64, 288, 384, 64, 1), (1, 144, 192, 64, 144, 192, 64, 0),
+         (1, 72, 96, 64, 144, 192, 64, 1), (1, 72, 96, 64, 72, 96, 64, 0)]
 L3 = [(1, 9, 12, 1280, 9, 12, 1280, 0), (1, 9, 12, 2560, 9, 12, 1280, 0), (1, 9, 12, 1280, 9, 12, 2560, 0),
       ("lin", 108, 1280, 1280), ("lin", 108, 2560, 1280), ("lin", 108, 1280, 2560), ("lin", 108, 10240, 1280),
       ("lin", 108, 5120, 1280), ("lin", 108, 3840, 1280)]
@@ -65,7 +68,7 @@ def main():
     ctx = Ctx(dev)
     nalg = _lib.load().dc_conv_num_algos()
     algos = args.algos or list(range(SKINNY_FIRST, nalg + 1))
-    shapes = {"l2": L2, "l3": L3, "all": L2 + L3}[args.set]
+    shapes = {"l2": L2, "l3": L3, "taesd": TAESD, "all": L2 + L3}[args.set]
     torch.manual_seed(0)
     for sh in shapes:
         if sh[0] == "lin":
