@@ -2,7 +2,7 @@ import csv, re, sys
 from collections import defaultdict
 def fam(n):
     n=n.replace("(anonymous namespace)::","")
-    for k in ("conv_gemm_kernel","conv_halo_kernel","conv_skinny_kernel","attn_fwd","attn_bwd_dq","attn_bwd_dkdv","gn_","ln_","cross_mfma","upsample","memset"):
+    for k in ("conv_gemm_kernel","conv_halo_kernel","conv_skinny_kernel","skinny_reduce","conv_resident_kernel","attn_fwd","attn_bwd_dq","attn_bwd_dkdv","gn_","ln_","cross_mfma","upsample","memset"):
         if k in n: return k
     return re.sub(r"[<(].*","",n)[:40]
 rows=[]

@@ -4,7 +4,7 @@ Run:   rocprofv3 --kernel-trace -d <dir> -o run --output-format csv -- python3 t
        python tools/step_profile.py --trace <dir>/run_kernel_trace.csv --descs <descs.json>
 The first form runs a C2 call (graph-replayed guided steps) and writes the conv launches of one step, in launch
 order, with their shapes and chosen variants.  The second (CPU) takes the last complete step of the trace, matches
-its conv dispatches (conv_gemm_kernel / conv_halo_kernel / conv_skinny_kernel) to those launches by order, and prints the time per shape
+its conv dispatches (conv_gemm / conv_halo / conv_skinny (+ skinny_reduce) / conv_resident kernels) to those launches by order, and prints the time per shape
 group -- the step's own cache state and launch order, unlike tools/conv_breakdown.py's warm replays.
 """
 import argparse
@@ -67,7 +67,15 @@ def analyse(trace, descs_path):
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    conv = [r for r in rows if any(k in r[2] for k in ("conv_gemm_kernel", "conv_halo_kernel", "conv_skinny_kernel"))]
+    # one entry per dc_conv_gemm launch: a two-kernel skinny split-K's reduce dispatch is added to its skinny kernel
+    conv = []
+    for r in rows:
+        if "skinny_reduce_kernel" in r[2] and conv:
+            s0, e0, n0 = conv[-1]
+            conv[-1] = (s0, e0 + (r[1] - r[0]), n0)
+        elif any(k in r[2] for k in ("conv_gemm_kernel", "conv_halo_kernel", "conv_skinny_kernel",
+                                     "conv_resident_kernel")):
+            conv.append(r)
     n = len(descs)
     last = conv[-n:]   # the final step of the last call is the last n conv dispatches (final decode is dense:
     # skip back over the final decode's convs by aligning on shapes below)
@@ -75,8 +83,9 @@ def analyse(trace, descs_path):
     best = None
     for off in range(0, min(len(conv) - n, 200) + 1):
         win = conv[len(conv) - n - off:len(conv) - off]
-        fam = lambda a: "halo" if 23 <= a <= 36 else ("skinny" if a >= 43 else "gemm")   # noqa: E731
-        ok = sum((fam(d["algo"]) in w[2]) or (fam(d["algo"]) == "skinny") for w, d in zip(win, descs))
+        fam = lambda a: ("halo" if 23 <= a <= 36 else "skinny" if 43 <= a <= 54 else "resident" if a >= 55  # noqa: E731
+                         else "gemm")
+        ok = sum(fam(d["algo"]) in w[2] for w, d in zip(win, descs))
         if best is None or ok > best[0]:
             best = (ok, win)
         if ok == n:
