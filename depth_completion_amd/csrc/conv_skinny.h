@@ -394,17 +394,32 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const ConvGemmParams
   const int n0 = tn * C::BN;
   const __amdgpu_buffer_rsrc_t rs = ws_rsrc(p.ws);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  // every split's partial of the lane's NJ fragments in flight at once (rounds of RK loads), summed in split order
+  constexpr int RK = 16;
+  f32x4 s[NJ];
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) s[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const long base = (long)lb * TILE_F + wid * WAVE_F + ii * NJ * 256 + lane * 4;
+  for (int k0 = 0; k0 < p.splits; k0 += RK) {
+    f32x4 part[RK][NJ];
+#pragma unroll
+    for (int k = 0; k < RK; ++k)
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj)
+        if (k0 + k < p.splits) part[k][jj] = load_sc1_x4(rs, base + (long)(k0 + k) * tiles * TILE_F + jj * 256);
+#pragma unroll
+    for (int k = 0; k < RK; ++k)
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj)
+        if (k0 + k < p.splits) s[jj] += part[k][jj];
+  }
 #pragma unroll
   for (int jj = 0; jj < NJ; ++jj) {
-    const long off = (long)lb * TILE_F + wid * WAVE_F + (ii * NJ + jj) * 256 + lane * 4;
-    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int k = 0; k < p.splits; ++k) s += load_sc1_x4(rs, off + (long)k * tiles * TILE_F);
     const int cl = wid * C::WN + jj * 16 + col_l;
     const int c = n0 + cl;
     const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) es[(row_l + e) * C::LDE + cl] = (bf16)(s[e] + bv);
+    for (int e = 0; e < 4; ++e) es[(row_l + e) * C::LDE + cl] = (bf16)(s[jj][e] + bv);
   }
   __syncthreads();
   if (p.diag & 64) return;
