@@ -10,8 +10,9 @@ int conv_launch_skinny1(int i, ConvGemmParams& p, int splits, hipStream_t s);
 int conv_launch_resident(int i, ConvGemmParams& p, int bpc, hipStream_t s);
 
 // external algo ids: 1 .. kNumAll im2col / halo variants (conv_gemm_impl.h), then the weight-streaming skinny variants,
-// then the weight-resident persistent narrow convs (conv_skinny.h)
-constexpr int kNumExt = kNumAll + kNumSkinny + kNumResident;
+// then the weight-resident persistent narrow convs (conv_skinny.h), then the wide im2col tiles (conv_gemm_impl.h)
+static_assert(kNumAll + kNumSkinny + kNumResident + 1 == kWideFirst, "external algo id blocks");
+constexpr int kNumExt = kWideFirst + kNumWide - 1;
 extern "C" int dc_conv_num_algos(void) { return kNumExt; }
 
 extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
@@ -61,7 +62,8 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.rowbias && !p.rowbias_idx) return DC_ERR_ARG;
   if (p.mode < 0 || p.mode > 2) return DC_ERR_ARG;
   if (p.mode == 2 && p.kh != 3) return DC_ERR_ARG;
-  if (d->algo < 0 || d->algo > kNumExt || d->splitk < (d->algo > kNumAll ? -32 : -4)) return DC_ERR_ARG;
+  if (d->algo < 0 || d->algo > kNumExt || d->splitk < ((d->algo > kNumAll && d->algo < kWideFirst) ? -32 : -4))
+    return DC_ERR_ARG;
   const bool smallc = (p.cin % 64) != 0;
   if (d->x2 && (smallc || p.c1 % 64 != 0)) return DC_ERR_ARG;
   if ((p.ldx | p.ldx2 | p.ldy) % 8 != 0) return DC_ERR_ALIGN;
@@ -121,13 +123,21 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
-  if (algo > kNumAll + kNumSkinny) {
+  if (algo >= kWideFirst) {
+    // wide im2col tile: the launch below (algo_index maps it into kAlgos).  No fused-GroupNorm form: a GroupNorm-fused
+    // call that carries a wide choice (the table's entry is shared with the shape's unfused calls, and a shape is
+    // tuned before its GroupNorm consumers register) runs the 64 x 64 double-buffered tile, the level-0 winner before
+    if (p.gn.mode != 0) {
+      algo = 13;
+      splits = 1;
+    }
+  } else if (algo > kNumAll + kNumSkinny) {
     const int ri = algo - kNumAll - kNumSkinny - 1;
     if (resident_eligible(p)) return conv_launch_resident(ri, p, splits, s);
     algo = 0;   // outside the narrow-conv contract (nearest-shape pick): im2col heuristic
     splits = 0;
   }
-  if (algo > kNumAll) {
+  if (algo > kNumAll && algo < kWideFirst) {
     const int si = algo - kNumAll - 1;
     if (skinny_eligible(p, si))
       return kSkinnyAlgos[si].kt == 9 ? conv_launch_skinny9(si, p, splits == 0 ? 1 : splits, s)

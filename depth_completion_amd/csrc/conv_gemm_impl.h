@@ -272,6 +272,7 @@ __device__ __forceinline__ void gn_epilogue_rows(const ConvGemmParams& p, char* 
   constexpr int GPR = WN / 8;
   constexpr int RMAX = (WM * GPR + 63) / 64;   // rows per lane
   static_assert(LDS >= 64 * 4 * 16 * 4 + 2 * BN * 4, "GroupNorm-statistics reduction LDS");
+  static_assert(64 % GPR == 0, "a lane's rows share one 8-channel column group");
   if (p.diag & 64) return;   // experiments only: no epilogue at all
   const GnFuseP& G = p.gn;
   const GnTargetP& t0 = G.t[0];
@@ -1296,16 +1297,27 @@ constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 
                            // (round 3, algo ids 37 ..) rings that fill the LDS of two blocks per CU (S = 5 at
                            // 64x64: the round-2 abort did not reproduce, profiles/r03p), or of three at 64x64 S = 3
                            {64, 64, 64, 5},    {128, 64, 64, 3},  {64, 128, 64, 3}, {64, 32, 64, 6},
-                           {128, 32, 64, 4},   {64, 64, 64, 3}};
+                           {128, 32, 64, 4},   {64, 64, 64, 3},
+                           // (round 3, algo ids 59 ..) wide tiles: all 320 output channels of a short-K linear / conv
+                           // in one block, so each A row is filled into LDS once instead of once per 64-wide column
+                           // tile (the level-0 attention projections, M = 6912, K = N = 320)
+                           {32, 320, 64, 2},   {64, 320, 64, 2},  {32, 320, 64, 3}};
 // External algo ids (dc_conv_desc.algo; the tuned table stores them): 1 .. kNumBase the first kNumBase entries of
 // kAlgos, kNumBase + 1 .. kNumBase + kNumHalo the halo variants, then the later kAlgos entries.
-constexpr int kNumAlgos = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1;
+constexpr int kNumAlgos = 28;   // kAlgos entries behind external ids 1 .. kNumAll (the wide tiles come after)
 constexpr int kNumBase = 22;
 constexpr int kNumHalo = sizeof(kHaloAlgos) / sizeof(kHaloAlgos[0]);
 constexpr int kNumAll = kNumAlgos + kNumHalo;
+// the wide tiles (kAlgos[kNumAlgos + 1 ..]) take the external ids after the skinny (43 .. 54) and resident (55 .. 58)
+// variants of conv_skinny.h (conv_gemm.hip checks the numbering)
+constexpr int kWideFirst = 59;
+constexpr int kNumWide = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1 - kNumAlgos;
+static_assert(kNumAll == 42, "external algo ids of the tuned tables");
 __host__ __device__ constexpr bool algo_is_halo(int id) { return id > kNumBase && id <= kNumBase + kNumHalo; }
-// kAlgos index of a non-halo external id
-__host__ __device__ constexpr int algo_index(int id) { return id <= kNumBase ? id : id - kNumHalo; }
+// kAlgos index of an im2col external id
+__host__ __device__ constexpr int algo_index(int id) {
+  return id <= kNumBase ? id : (id <= kNumAll ? id - kNumHalo : id - kWideFirst + kNumAlgos + 1);
+}
 static_assert(kNumHalo == 14, "DC_HALO cases below");
 
 template <int TH, int TW, int BN, int WGM, int WGN, int S, int SCHED, int GNM>
@@ -1421,6 +1433,14 @@ int launch_algo_idx(int algo, ConvGemmParams& p, long M, int splits, bool smallc
     DC_ALGO(1) DC_ALGO(2) DC_ALGO(3) DC_ALGO(4) DC_ALGO(5) DC_ALGO(6) DC_ALGO(7) DC_ALGO(8) DC_ALGO(9) DC_ALGO(10)
     DC_ALGO(11) DC_ALGO(12) DC_ALGO(13) DC_ALGO(14) DC_ALGO(15) DC_ALGO(16) DC_ALGO(17) DC_ALGO(18) DC_ALGO(19)
     DC_ALGO(20) DC_ALGO(21) DC_ALGO(22) DC_ALGO(23) DC_ALGO(24) DC_ALGO(25) DC_ALGO(26) DC_ALGO(27) DC_ALGO(28)
+#define DC_ALGO_WIDE(i)                                                                                        \
+  case i:                                                                                                      \
+    if constexpr (GNM == 0)                                                                                    \
+      return launch_algo<kAlgos[i].bm, kAlgos[i].bn, kAlgos[i].bk, kAlgos[i].s, 0>(p, M, splits, smallc, s); \
+    return DC_ERR_ARG;
+    // the wide tiles have no fused-GroupNorm form (gn_epilogue_rows needs 64 % (WN / 8) == 0; WN = 160 here)
+    DC_ALGO_WIDE(29) DC_ALGO_WIDE(30) DC_ALGO_WIDE(31)
+#undef DC_ALGO_WIDE
 #undef DC_ALGO
     default: return DC_ERR_ARG;
   }

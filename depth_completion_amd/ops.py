@@ -190,8 +190,9 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
 HALO_FIRST, HALO_LAST = 23, 36   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv (conv_gemm_impl.h); ids
 # 1 .. 22 and 37 .. 42 are im2col tile variants, SKINNY_FIRST .. dc_conv_num_algos() the weight-streaming skinny
 # conv / linear variants (conv_skinny.h)
-IM2COL_LAST, SKINNY_FIRST, RESIDENT_FIRST = 42, 43, 55   # RESIDENT_FIRST ..: the weight-resident persistent
-# narrow convs (cin 64, cout <= 64; their split field is the persistent grid's blocks per CU)
+IM2COL_LAST, SKINNY_FIRST, RESIDENT_FIRST, WIDE_FIRST = 42, 43, 55, 59   # RESIDENT_FIRST ..: the weight-resident
+# persistent narrow convs (cin 64, cout <= 64; their split field is the persistent grid's blocks per CU); WIDE_FIRST ..
+# dc_conv_num_algos(): im2col tiles holding 320 output channels per block
 SKINNY_TAPS = (9, 9, 9, 9, 9, 1, 1, 1, 1, 1, 1, 1)   # taps of skinny variant SKINNY_FIRST + i (conv_skinny.h kSkinnyAlgos)
 
 
@@ -235,7 +236,7 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     nalg = _lib.load().dc_conv_num_algos()
     # im2col tiles: split-K 1..32, and stream-K over 256 / 512 / 768 blocks (splitk -1 / -2 / -3); halo tiles
     # (algos > HALO_FIRST - 1, stride-1 3x3 convs over whole 64-channel chunks only): input-chunk splits
-    gemm_ids = list(range(1, HALO_FIRST)) + list(range(HALO_LAST + 1, IM2COL_LAST + 1))
+    gemm_ids = list(range(1, HALO_FIRST)) + list(range(HALO_LAST + 1, IM2COL_LAST + 1)) + list(range(WIDE_FIRST, nalg + 1))
     cands = [(0, 0)] + [(a, s) for a in gemm_ids for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
     if halo_eligible(d):
         cands += [(a, s) for a in range(HALO_FIRST, HALO_LAST + 1) for s in (1, 2, 3, 4, 5, 8, 10, 16, 20)
@@ -251,7 +252,7 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
         cur = ctx.tune_only[1].get(conv_key(d))
         cands = ([cur] if cur else []) + [c for c in cands if c[0] in ctx.tune_only[0]]
     if halo_eligible(d) and d.cin == 64 and d.cout <= 64 and not d.gn and not d.x2:
-        cands += [(a, b) for a in range(RESIDENT_FIRST, nalg + 1) for b in (0, 1, 2, 3)]
+        cands += [(a, b) for a in range(RESIDENT_FIRST, WIDE_FIRST) for b in (0, 1, 2, 3)]
     best, best_t = (0, 0), float("inf")
     # DC_TUNE_COLD=1: every timed call starts with L2 and the Infinity Cache flushed (a 512 MiB write),
     # as the weights are in the sampler step (each is touched once per pass)

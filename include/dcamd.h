@@ -101,8 +101,13 @@ typedef struct dc_conv_desc {
   int ldy2;
   const void* aux;
   int ldaux;
-  int algo;        /* 0 = heuristic, 1..dc_conv_num_algos(): tile/ring variant (plan-time autotuned) */
-  int splitk;      /* 0 = heuristic, >=1 explicit K split, -1..-4 stream-K over 256..1024 blocks (needs ws) */
+  int algo;        /* 0 = heuristic, 1..dc_conv_num_algos(): tile/ring variant (plan-time autotuned):
+                      1-22, 37-42, 59-61 im2col tiles; 23-36 halo-tile direct 3x3; 43-54 weight-streaming skinny
+                      conv / linear (few output pixels); 55-58 weight-resident persistent 3x3 (cin 64, cout <= 64).
+                      A variant given a shape outside its contract runs the heuristic. */
+  int splitk;      /* 0 = heuristic, >=1 explicit K split, -1..-4 stream-K over 256..1024 blocks (needs ws);
+                      skinny variants: -2..-32 = that K split summed by a second (reduce) kernel; resident variants:
+                      blocks per CU of the persistent grid (0 = as many as fit) */
   /* optional row list: only the nrows output pixels rows[0..nrows) (sorted indices into the nb*hout*wout
    * output rows) are computed and written; the others are left untouched (no GEGLU epilogue) */
   const int* rows;

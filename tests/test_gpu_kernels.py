@@ -493,7 +493,8 @@ def test_geglu_and_upsample_adjoint(ctx):
         assert rel(nchw(out, 2, hl, wl), x.grad) < 1e-2
 
 
-@pytest.mark.parametrize("algo", list(range(1, 23)) + list(range(37, 43)))   # the im2col ids (23 .. 36: halo)
+@pytest.mark.parametrize("algo", list(range(1, 23)) + list(range(37, 43)) + list(range(59, 62)))   # the im2col ids
+# (23 .. 36: halo, 43 .. 58: skinny / resident, 59 ..: wide tiles)
 @pytest.mark.parametrize("nsplit", [1, 3, -1, -2])
 def test_conv_all_algos(ctx, algo, nsplit):
     """every tile / ring variant, split-K (nsplit > 1) and stream-K (nsplit < 0: 256 / 512 blocks over
@@ -536,7 +537,7 @@ def test_conv_halo_algos(ctx, algo, nsplit):
     ReLU-backward mask) vs torch fp32 on the bf16 values; bitwise reproducible run to run."""
     from depth_completion_amd import ops
     from depth_completion_amd.weights import pack_conv
-    assert _lib_num_algos() == RESIDENT_LAST
+    assert _lib_num_algos() == NUM_ALGOS
     cases = [  # n, c1, c2, cout, h, w, mode, epilogue
         (2, 128, 64, 96, 9, 35, 0, True), (1, 64, 0, 64, 18, 24, 1, False), (1, 320, 0, 320, 9, 12, 0, True),
         (1, 64, 0, 32, 13, 70, 0, False)]
@@ -575,6 +576,7 @@ def test_conv_halo_algos(ctx, algo, nsplit):
 SKINNY_FIRST, SKINNY_LAST = 43, 54   # dc_conv_gemm algo ids of the weight-streaming skinny variants (conv_skinny.h)
 SKINNY_ALGOS = list(range(SKINNY_FIRST, SKINNY_LAST + 1))
 RESIDENT_FIRST, RESIDENT_LAST = 55, 58   # ... of the weight-resident persistent narrow convs (conv_skinny.h)
+NUM_ALGOS = 61   # dc_conv_num_algos(): ... and the wide im2col tiles 59 .. 61 (conv_gemm_impl.h)
 
 
 @pytest.mark.parametrize("algo", list(range(RESIDENT_FIRST, RESIDENT_LAST + 1)))
