@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -36,6 +36,12 @@ class GnFuse(C.Structure):
     ]
 
 
+class LnFuse(C.Structure):
+    """Mirror of ``dc_ln_fuse``: a LayerNorm of the input rows folded into a linear."""
+
+    _fields_ = [("csum", vp), ("cbias", vp), ("stats", vp)]
+
+
 class ConvDesc(C.Structure):
     """Mirror of ``dc_conv_desc`` (include/dcamd.h)."""
 
@@ -51,6 +57,7 @@ class ConvDesc(C.Structure):
         ("ws", vp), ("ws_bytes", i64),
         ("geglu", i32), ("y2", vp), ("ldy2", i32), ("aux", vp), ("ldaux", i32),
         ("algo", i32), ("splitk", i32), ("rows", vp), ("nrows", i32), ("gn", C.POINTER(GnFuse)),
+        ("ln", C.POINTER(LnFuse)),
     ]
 
 
@@ -75,8 +82,9 @@ _SIGS = {
     "dc_attn_bwd": [vp, i32, vp, i32, vp, i32, vp, i32, i32, i32, vp, vp, i32, vp, i64, vp],
     "dc_crossattn_tables_bytes": [i32, i32],
     "dc_crossattn_prepare": [vp, vp, i32, i32, vp, vp],
-    "dc_crossattn_fwd": [vp, i32, i64, i32, i32, f32, vp, vp, vp, vp, vp, i32, vp, vp, vp],
+    "dc_crossattn_fwd": [vp, i32, i64, i32, i32, f32, vp, vp, vp, vp, vp, i32, vp, vp, vp, f32, vp],
     "dc_crossattn_bwd": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, i32, vp, i32, vp],
+    "dc_crossattn_bwd_ln": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, i32, vp, i32, vp, vp, i32, vp, i32, vp],
     "dc_geglu_fwd": [vp, i32, i64, i32, vp, i32, vp],
     "dc_geglu_bwd": [vp, i32, i64, i32, vp, i32, vp, i32, vp],
     "dc_upsample_adjoint": [vp, i32, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, vp],
@@ -125,6 +133,7 @@ _SIGS.update({
     "dc_schedule_tables": [i32, C.c_double, C.c_double, i32, vp, vp, vp],
     "dc_timestep_embedding": [vp, i32, i32, vp],
     "dc_fold_cross_attention": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+    "dc_fold_layernorm": [vp, i32, i32, vp, vp, vp, vp, vp, vp],
     "dc_conv_pick": [vp, vp, i32, vp, vp],
     "dc_sample_params_default": [vp],
     "dc_latent_hw": [i32, i32, i32, vp, vp],

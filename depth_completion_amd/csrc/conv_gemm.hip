@@ -123,6 +123,29 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   int algo = d->algo, splits = d->splitk;
+  p.ln_csum = nullptr;
+  p.ln_cbias = nullptr;
+  p.ln_stats = nullptr;
+  if (d->ln) {
+    // LayerNorm folded in (dc_ln_fuse): a linear on an im2col tile (split-K / stream-K allowed: the epilogue
+    // applies the row statistics to the summed tile)
+    const dc_ln_fuse& l = *d->ln;
+    if (!l.csum || !l.cbias || !l.stats || p.bias || p.gn.mode || p.rows || d->x2 || p.geglu > 1 || p.kh != 1 ||
+        p.kw != 1 || p.stride != 1 || p.pad != 0 || p.mode != 0 || p.cin != p.ktot || p.hin != p.hout ||
+        p.win != p.wout)
+      return DC_ERR_ARG;
+    p.ln_csum = l.csum;
+    p.ln_cbias = l.cbias;
+    p.ln_stats = l.stats;
+    const bool im2col = (algo >= 1 && algo <= kNumBase) || (algo > kNumBase + kNumHalo && algo <= kNumAll);
+    if (!im2col || splits == 0) {   // a halo / skinny / resident / wide choice, or none: the im2col heuristic
+      int a2, s2;
+      auto_algo(M, p.cout, p.ktot / 64, a2, s2);
+      if (!im2col) algo = a2;
+      splits = (!im2col || splits == 0) ? s2 : splits;
+    }
+    return conv_launch_algo_ln(algo_index(algo), p, M, splits, smallc, s);
+  }
   if (algo >= kWideFirst) {
     // wide im2col tile: the launch below (algo_index maps it into kAlgos).  No fused-GroupNorm form: a GroupNorm-fused
     // call that carries a wide choice (the table's entry is shared with the shape's unfused calls, and a shape is

@@ -88,6 +88,11 @@ struct ConvGemmParams {
   unsigned hw_mul, w_mul, h_mul;
   int hw_shr, w_shr, h_shr;
   GnFuseP gn;
+  // LayerNorm of the A rows folded into a linear (dc_ln_fuse; the GNM == 3 instantiations): the epilogue applies
+  // y = rstd (acc - mean csum[n]) + cbias[n] with the rows' (mean, rstd) from ln_stats
+  const float* ln_csum;
+  const float* ln_cbias;
+  const float* ln_stats;
 };
 
 // x / d for x < 2^31 by a host-computed (mul, shr) pair (make_fast_div); mul == 0 encodes d == 1
@@ -786,14 +791,39 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
   constexpr int LDE = WN + 8;
   bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
   DC_LDS_ASSERT((wid * WM * LDE) * 2, WM * LDE * 2, (Cfg<BM, BN, 64, 2>::EPI));
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int c = n0 + wn * WN + j * 16 + col_l;
-    const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+  if constexpr (GNM == 3) {
+    // LayerNorm folded in: y = rstd (acc - mean csum[c]) + cbias[c], the rows' (mean, rstd) from p.ln_stats
+    float mu[MI][4], rs[MI][4];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) es[(i * 16 + row_l + e) * LDE + j * 16 + col_l] = (bf16)(acc[i][j][e] + bv);
+      for (int e = 0; e < 4; ++e) {
+        const long m = m0 + wm * WM + i * 16 + row_l + e;
+        const bool in = m < M;
+        mu[i][e] = in ? p.ln_stats[m * 2] : 0.0f;
+        rs[i][e] = in ? p.ln_stats[m * 2 + 1] : 0.0f;
+      }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = n0 + wn * WN + j * 16 + col_l;
+      const float cs = c < p.cout ? p.ln_csum[c] : 0.0f;
+      const float cb = c < p.cout ? p.ln_cbias[c] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          es[(i * 16 + row_l + e) * LDE + j * 16 + col_l] = (bf16)(rs[i][e] * (acc[i][j][e] - mu[i][e] * cs) + cb);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = n0 + wn * WN + j * 16 + col_l;
+      const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) es[(i * 16 + row_l + e) * LDE + j * 16 + col_l] = (bf16)(acc[i][j][e] + bv);
+    }
   }
   __builtin_amdgcn_wave_barrier();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -842,7 +872,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
     }
     return;
   }
-  if constexpr (GNM != 0) {
+  if constexpr (GNM == 1 || GNM == 2) {
     // frames of the block's first and last row decide the block-uniform reduction form
     const long mA = m0 + wm * WM;
     const long mlast = min(M, m0 + BM) - 1;
@@ -883,6 +913,7 @@ template <int BM, int BN, int BK, int S, bool SMALLC, bool SK, int GNM>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, BK, S>::LDS];
   f32x4 acc[BM / 32][BN / 32];
+  if (p.diag & 128) return;   // experiments only: the launch and dispatch alone (tools/launch_floor.py)
   const int tiles_n = (p.cout + BN - 1) / BN;
   const int nk = p.ktot / BK;
 
@@ -1453,3 +1484,5 @@ int conv_launch_halo_gn(int i, ConvGemmParams& p, int splits, hipStream_t s);
 int conv_launch_algo_gn(int algo, ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t s);
 int conv_launch_halo_gnb(int i, ConvGemmParams& p, int splits, hipStream_t s);
 int conv_launch_algo_gnb(int algo, ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t s);
+// the LayerNorm-folded instantiations (conv_gemm_ln.hip: im2col tiles)
+int conv_launch_algo_ln(int algo, ConvGemmParams& p, long M, int splits, bool smallc, hipStream_t s);

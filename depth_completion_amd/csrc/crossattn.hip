@@ -138,7 +138,7 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, int ldx, long rows, int c, int heads,
                                                                  float eps, const float* gamma, const float* beta,
                                                                  const bf16* tabs, const float* c0, bf16* y, int ldy,
-                                                                 float* stats, float* probs) {
+                                                                 float* stats, float* probs, float* ystats, float yeps) {
   constexpr int MK = Fit<NW>::MK, MCT = Fit<NW>::MCT;
   __shared__ float s_red[NW][kRows];
   __shared__ float s_part[NW][kRows][kHP + 1];
@@ -242,9 +242,12 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, 
     for (int j = 0; j < 8; ++j) v[j] = s_sig[r][g * 8 + j];
     split8(v, sh, sl);
   }
+  float yv[MCT][4];   // the stored output values of the lane's row segments (norm3's statistics below)
 #pragma unroll
   for (int t = 0; t < MCT; ++t) {
     const int ct = cb + t;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) yv[t][j] = 0.0f;
     if (ct < ce) {
       f32x4 o = {0.f, 0.f, 0.f, 0.f};
       o = mfma(sh, bt[t][0], o);
@@ -257,24 +260,117 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, 
       if (orow < rows) {
         bf16x4 ov;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) ov[j] = (bf16)(s_tile[w][rr][cc + j] + (float)xres[t][j]);
+        for (int j = 0; j < 4; ++j) {
+          ov[j] = (bf16)(s_tile[w][rr][cc + j] + (float)xres[t][j]);
+          yv[t][j] = (float)ov[j];
+        }
         *reinterpret_cast<bf16x4*>(y + orow * ldy + ct * 16 + cc) = ov;
       }
       __builtin_amdgcn_wave_barrier();
     }
   }
+  if (ystats) {
+    // (mean, rstd) of each output row (the next LayerNorm's statistics, dc_ln_fuse): two passes over the stored
+    // values, the 4 lanes of a row then the waves in order
+    float sm = 0.0f;
+#pragma unroll
+    for (int t = 0; t < MCT; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sm += yv[t][j];
+    sm += __shfl_xor(sm, 1, 64);
+    sm += __shfl_xor(sm, 2, 64);
+    __syncthreads();
+    if ((lane & 3) == 0) s_red[w][rr] = sm;
+    __syncthreads();
+    float tot = 0.0f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) tot += s_red[v][rr];
+    const float ym = tot / c;
+    float q = 0.0f;
+#pragma unroll
+    for (int t = 0; t < MCT; ++t)
+      if (cb + t < ce)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = yv[t][j] - ym;
+          q += d * d;
+        }
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    __syncthreads();
+    if ((lane & 3) == 0) s_red[w][rr] = q;
+    __syncthreads();
+    tot = 0.0f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) tot += s_red[v][rr];
+    if (w == 0 && (lane & 3) == 0 && orow < rows) {
+      ystats[orow * 2] = ym;
+      ystats[orow * 2 + 1] = rsqrtf(tot / c + yeps);
+    }
+  }
 }
 
-template <int NW>
+// The LayerNorm (norm3) backward that produces this kernel's dy, fused in front of it (LN3 = true): dy = LN3bwd(dl) +
+// add for the block's 16 rows into an LDS tile, one wave per row, with the arithmetic (and summation order) of
+// norms.hip ln_bwd_kernel with gamma folded into dl (dc_ln_fuse) -- the same bits as the two-launch form.
+struct Ln3Bwd {
+  const bf16* dl;
+  int lddl;
+  const bf16* x3;   // norm3's input (r2)
+  int ldx3;
+  const float* stats3;
+  const bf16* add;
+  int ldadd;
+};
+constexpr int kDyLd = kMaxC + 8;   // LDS row stride of the dy tile (bf16; 16-B pad against bank conflicts)
+
+template <int MAXV>
+__device__ __forceinline__ void ln3_bwd_row(const Ln3Bwd& L, long row, int c, int lane, bf16* out) {
+  const int nv = c >> 3;
+  const float mu = L.stats3[row * 2], rs = L.stats3[row * 2 + 1];
+  float xh[MAXV][8], gg[MAXV][8];
+  float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nv) {
+      float f[8], d[8];
+      load8(L.x3 + row * L.ldx3 + vi * 8, f);
+      load8(L.dl + row * L.lddl + vi * 8, d);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        xh[k][i] = (f[i] - mu) * rs;
+        gg[k][i] = d[i];
+        sa += gg[k][i];
+        sb += gg[k][i] * xh[k][i];
+      }
+    }
+  }
+  const float ma = wave_sum(sa) / c, mb = wave_sum(sb) / c;
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vi = lane + 64 * k;
+    if (vi < nv) {
+      float o[8], e[8];
+      load8(L.add + row * L.ldadd + vi * 8, e);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)(rs * (gg[k][i] - ma - xh[k][i] * mb)) + e[i];
+      store8(out + vi * 8, o);
+    }
+  }
+}
+
+template <int NW, bool LN3>
 __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, int ldx, long rows, int c, int heads,
                                                                  const float* gamma, const bf16* tabs,
                                                                  const float* stats, const float* probs, const bf16* dy,
-                                                                 int lddy, bf16* dx, int lddx) {
+                                                                 int lddy, bf16* dx, int lddx, Ln3Bwd ln3) {
   constexpr int MK = Fit<NW>::MK, MCT = Fit<NW>::MCT;
   __shared__ float s_part[NW][kRows][kHP + 1];
   __shared__ float s_sig[kRows][kHP + 4];
   __shared__ float s_red[NW][kRows][2];
   __shared__ float s_tile[NW][kRows][17];
+  __shared__ __attribute__((aligned(16))) bf16 s_dy[LN3 ? kRows : 1][LN3 ? kDyLd : 8];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const long row0 = (long)blockIdx.x * kRows;
   const long row = row0 + r;
@@ -284,12 +380,27 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
   const int rr = lane >> 2, cc = (lane & 3) * 4;
   const long orow = row0 + rr;
   const Tabs T(tabs, c);
+  if constexpr (LN3) {
+    // phase 0: dy of the block's rows (norm3 backward + residual) into the LDS tile
+    for (int q = w; q < kRows; q += NW) {
+      if (row0 + q < rows) {
+        if ((c >> 3) <= 64) ln3_bwd_row<1>(ln3, row0 + q, c, lane, &s_dy[q][0]);
+        else ln3_bwd_row<3>(ln3, row0 + q, c, lane, &s_dy[q][0]);
+      }
+    }
+    __syncthreads();
+  }
+  // dy row r / rr of the block: the LDS tile (LN3) or global memory
+  auto dy_at = [&](int rl, long rg, int col) -> const bf16* {
+    if constexpr (LN3) return &s_dy[rl][col];
+    else return dy + rg * lddy + col;
+  };
   // phase 1: G = dy . D^T over the wave's channel chunks (dy is exactly bf16)
   bf16x8 av[MK];
 #pragma unroll
   for (int i = 0; i < MK; ++i) {
     if (kb + i < ke && ok) {
-      av[i] = ld8(dy + row * lddy + (kb + i) * 32 + g * 8);
+      av[i] = ld8(dy_at(r, row, (kb + i) * 32 + g * 8));
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) av[i][j] = (bf16)0.0f;
@@ -307,7 +418,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
   for (int t = 0; t < MCT; ++t)
     if (cb + t < ce && orow < rows) {
       xw[t] = *reinterpret_cast<const bf16x4*>(x + orow * ldx + (cb + t) * 16 + cc);
-      dyw[t] = *reinterpret_cast<const bf16x4*>(dy + orow * lddy + (cb + t) * 16 + cc);
+      dyw[t] = *reinterpret_cast<const bf16x4*>(dy_at(rr, orow, (cb + t) * 16 + cc));
     }
   const float mu = orow < rows ? stats[orow * 2] : 0.0f;
   const float rs = orow < rows ? stats[orow * 2 + 1] : 0.0f;
@@ -419,7 +530,7 @@ extern "C" int dc_crossattn_prepare(const float* U, const float* D, int heads, i
 
 extern "C" int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps,
                                 const float* gamma, const float* beta, const void* tabs, const float* c0, void* y,
-                                int ldy, float* stats, float* probs, void* stream) {
+                                int ldy, float* stats, float* probs, float* ystats, float yeps, void* stream) {
   if (!x || !y || !gamma || !beta || !tabs || !c0 || !stats || !probs || rows <= 0 || heads <= 0 || heads > kHP ||
       c % 32 || c > kMaxC)
     return DC_ERR_ARG;
@@ -427,13 +538,34 @@ extern "C" int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, i
   const dim3 grid((unsigned)((rows + kRows - 1) / kRows));
   if (cross_waves(c) == 8)
     hipLaunchKernelGGL(cross_mfma_fwd_kernel<8>, grid, dim3(512), 0, (hipStream_t)stream, (const bf16*)x, ldx,
-                       (long)rows, c, heads, eps, gamma, beta, (const bf16*)tabs, c0, (bf16*)y, ldy, stats, probs);
+                       (long)rows, c, heads, eps, gamma, beta, (const bf16*)tabs, c0, (bf16*)y, ldy, stats, probs,
+                       ystats, yeps);
   else
     hipLaunchKernelGGL(cross_mfma_fwd_kernel<16>, grid, dim3(1024), 0, (hipStream_t)stream, (const bf16*)x, ldx,
-                       (long)rows, c, heads, eps, gamma, beta, (const bf16*)tabs, c0, (bf16*)y, ldy, stats, probs);
+                       (long)rows, c, heads, eps, gamma, beta, (const bf16*)tabs, c0, (bf16*)y, ldy, stats, probs,
+                       ystats, yeps);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
+
+namespace {
+template <bool LN3>
+int cross_bwd_launch(const void* x, int ldx, long long rows, int c, int heads, const float* gamma, const void* tabs,
+                     const float* stats, const float* probs, const void* dy, int lddy, void* dx, int lddx,
+                     const Ln3Bwd& ln3, void* stream) {
+  const dim3 grid((unsigned)((rows + kRows - 1) / kRows));
+  if (cross_waves(c) == 8)
+    hipLaunchKernelGGL((cross_mfma_bwd_kernel<8, LN3>), grid, dim3(512), 0, (hipStream_t)stream, (const bf16*)x, ldx,
+                       (long)rows, c, heads, gamma, (const bf16*)tabs, stats, probs, (const bf16*)dy, lddy, (bf16*)dx,
+                       lddx, ln3);
+  else
+    hipLaunchKernelGGL((cross_mfma_bwd_kernel<16, LN3>), grid, dim3(1024), 0, (hipStream_t)stream, (const bf16*)x,
+                       ldx, (long)rows, c, heads, gamma, (const bf16*)tabs, stats, probs, (const bf16*)dy, lddy,
+                       (bf16*)dx, lddx, ln3);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}
+}  // namespace
 
 extern "C" int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, int heads, const float* gamma,
                                 const void* tabs, const float* stats, const float* probs, const void* dy, int lddy,
@@ -443,15 +575,20 @@ extern "C" int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, i
     return DC_ERR_ARG;
   if (ldx % 8 || lddy % 8 || lddx % 8 || ((uintptr_t)dy & 15) || ((uintptr_t)x & 7) || ((uintptr_t)dx & 7))
     return DC_ERR_ALIGN;
-  const dim3 grid((unsigned)((rows + kRows - 1) / kRows));
-  if (cross_waves(c) == 8)
-    hipLaunchKernelGGL(cross_mfma_bwd_kernel<8>, grid, dim3(512), 0, (hipStream_t)stream, (const bf16*)x, ldx,
-                       (long)rows, c, heads, gamma, (const bf16*)tabs, stats, probs, (const bf16*)dy, lddy, (bf16*)dx,
-                       lddx);
-  else
-    hipLaunchKernelGGL(cross_mfma_bwd_kernel<16>, grid, dim3(1024), 0, (hipStream_t)stream, (const bf16*)x, ldx,
-                       (long)rows, c, heads, gamma, (const bf16*)tabs, stats, probs, (const bf16*)dy, lddy, (bf16*)dx,
-                       lddx);
-  DC_CHECK_LAUNCH();
-  return DC_OK;
+  return cross_bwd_launch<false>(x, ldx, rows, c, heads, gamma, tabs, stats, probs, dy, lddy, dx, lddx, Ln3Bwd{},
+                                 stream);
+}
+
+extern "C" int dc_crossattn_bwd_ln(const void* x, int ldx, long long rows, int c, int heads, const float* gamma,
+                                   const void* tabs, const float* stats, const float* probs, const void* dl, int lddl,
+                                   const void* x3, int ldx3, const float* stats3, const void* add, int ldadd, void* dx,
+                                   int lddx, void* stream) {
+  if (!x || !dl || !x3 || !stats3 || !add || !dx || !gamma || !tabs || !stats || !probs || rows <= 0 || heads <= 0 ||
+      heads > kHP || c % 32 || c > kMaxC)
+    return DC_ERR_ARG;
+  if (ldx % 8 || lddl % 8 || ldx3 % 8 || ldadd % 8 || lddx % 8 || ((uintptr_t)dl & 15) || ((uintptr_t)x3 & 15) ||
+      ((uintptr_t)add & 15) || ((uintptr_t)x & 7) || ((uintptr_t)dx & 7))
+    return DC_ERR_ALIGN;
+  const Ln3Bwd ln3{(const bf16*)dl, lddl, (const bf16*)x3, ldx3, stats3, (const bf16*)add, ldadd};
+  return cross_bwd_launch<true>(x, ldx, rows, c, heads, gamma, tabs, stats, probs, nullptr, 0, dx, lddx, ln3, stream);
 }

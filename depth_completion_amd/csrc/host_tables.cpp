@@ -6,6 +6,7 @@
 //                            reduced to per-step scalars, and torch.optim.Adam's bias corrections (:783, 897)
 //   dc_timestep_embedding    diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), fp32
 //   dc_fold_cross_attention  attn2 with the constant 2-token empty-prompt context folded to (U, D, c0)
+//   dc_fold_layernorm        a LayerNorm folded into the linear that consumes it (include/dcamd.h dc_ln_fuse)
 //   dc_conv_pick             the tuned GEMM variant of a conv shape, nearest tuned shape for shapes not in the table
 #include <cmath>
 #include <cstdint>
@@ -95,6 +96,30 @@ extern "C" int dc_timestep_embedding(const long long* timesteps, int n, int dim,
       out[(long)r * dim + i] = std::cos(e);          // flip_sin_to_cos: [cos | sin]
       out[(long)r * dim + half + i] = std::sin(e);
     }
+  }
+  return 0;
+}
+
+extern "C" int dc_fold_layernorm(const float* w, int cout, int k, const float* gamma, const float* beta,
+                                 const float* bias, void* wf, float* csum, float* cbias) {
+  // W' = bf16(W[n][k] gamma[k]); csum[n] = sum_k W'[n][k] (of the rounded W', so that the kernel's
+  // x . W' - mean csum equals (x - mean) . W' up to fp32 rounding); cbias[n] = sum_k W[n][k] beta[k] + bias[n]
+  // (double, in k order: both hosts get the same bits)
+  if (!w || !gamma || !beta || !wf || !csum || !cbias || cout <= 0 || k <= 0) return 1;
+  uint16_t* o = static_cast<uint16_t*>(wf);
+  for (int n = 0; n < cout; ++n) {
+    double cs = 0.0, cb = 0.0;
+    for (int i = 0; i < k; ++i) {
+      const float wv = round_bf16(w[(size_t)n * k + i]);
+      const float f = round_bf16(wv * round_bf16(gamma[i]));
+      uint32_t u;
+      memcpy(&u, &f, 4);
+      o[(size_t)n * k + i] = (uint16_t)(u >> 16);
+      cs += (double)f;
+      cb += (double)wv * (double)round_bf16(beta[i]);
+    }
+    csum[n] = (float)cs;
+    cbias[n] = (float)(cb + (bias ? (double)round_bf16(bias[n]) : 0.0));
   }
   return 0;
 }

@@ -897,7 +897,7 @@ __global__ void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const fl
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         xh[k][i] = (f[i] - mu) * rs;
-        g[k][i] = d[i] * gamma[vi * 8 + i];
+        g[k][i] = gamma ? d[i] * gamma[vi * 8 + i] : d[i];   // gamma NULL: dy is gamma * dL/dy already
         sa += g[k][i];
         sb += g[k][i] * xh[k][i];
       }
@@ -950,7 +950,7 @@ extern "C" int dc_layernorm_fwd(const void* x, int ldx, long long rows, int c, f
 extern "C" int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, const float* gamma, const float* stats,
                                 const void* dy, int lddy, void* dx, int lddx, const void* add, int ldadd,
                                 void* stream) {
-  if (!x || !dy || !dx || !gamma || !stats || rows <= 0 || c <= 0 || c % 8) return DC_ERR_ARG;
+  if (!x || !dy || !dx || !stats || rows <= 0 || c <= 0 || c % 8) return DC_ERR_ARG;
   if (ldx % 8 || lddy % 8 || lddx % 8 || (add && ldadd % 8)) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   const int wpb = 4;

@@ -160,6 +160,10 @@ struct LinearW {
   void* wf = nullptr;  // [cout][cin]
   void* wd = nullptr;  // [cin][cout]
   float* bias = nullptr;
+  // a LayerNorm folded in (weights.LnLinear, dc_ln_fuse): wf / wd are the gamma-scaled weights, bias is NULL
+  float* csum = nullptr;
+  float* cbias = nullptr;
+  float eps = 0.0f;
 };
 
 struct NormW {
@@ -229,6 +233,26 @@ class Loader {
     }
     return l;
   }
+  // weights.LnLinear: the LayerNorm `norm_pre` folded into the linear (the shared host routine dc_fold_layernorm)
+  LinearW linear_ln_from(HostTensor w, const float* b, const std::string& norm_pre, float eps) {
+    HostTensor g = st_.get(norm_pre + ".weight"), be = st_.get(norm_pre + ".bias");
+    LinearW l;
+    l.cout = (int)w.shape[0];
+    l.cin = (int)w.shape[1];
+    l.eps = eps;
+    std::vector<uint16_t> wf((size_t)l.cout * l.cin);
+    std::vector<float> cs(l.cout), cb(l.cout);
+    DCK(dc_fold_layernorm(w.data.data(), l.cout, l.cin, g.data.data(), be.data.data(), b, wf.data(), cs.data(),
+                          cb.data()));
+    l.wf = mem_.upload(wf);
+    std::vector<uint16_t> t((size_t)l.cin * l.cout);
+    for (int o = 0; o < l.cout; ++o)
+      for (int i = 0; i < l.cin; ++i) t[(size_t)i * l.cout + o] = wf[(size_t)o * l.cin + i];
+    l.wd = mem_.upload(t);
+    l.csum = mem_.upload(cs);
+    l.cbias = mem_.upload(cb);
+    return l;
+  }
   LinearW linear(const std::string& pre, bool has_bias, bool dgrad = true) {
     HostTensor w = st_.get(pre + ".weight");
     HostTensor b;
@@ -288,6 +312,7 @@ struct Exec {
     const int* rows = nullptr;
     int nrows = 0;
     const dc_gn_fuse* gn = nullptr;   // fused GroupNorm statistics (unet.py _gnf / _gn_bwd_fuse)
+    const dc_ln_fuse* ln = nullptr;   // LayerNorm folded in (unet.py ln_fuse)
   };
   void conv(const Conv& a) {
     dc_conv_desc d;
@@ -321,6 +346,7 @@ struct Exec {
     d.ws = ws;
     d.ws_bytes = ws_bytes;
     d.gn = a.gn;
+    d.ln = a.ln;
     if (a.rows) {
       d.rows = a.rows;
       d.nrows = a.nrows;
@@ -348,7 +374,7 @@ struct Exec {
   // ops.linear
   void linear(RB x, const void* w, int k, int rows, int cout, RB y, const float* bias = nullptr, RB resid = RB(),
               const void* rowbias = nullptr, int rowbias_ld = 0, int geglu = 0, RB y2 = RB(), RB aux = RB(),
-              const dc_gn_fuse* gn = nullptr) {
+              const dc_gn_fuse* gn = nullptr, const dc_ln_fuse* ln = nullptr) {
     Conv a;
     a.x = x;
     a.nb = 1; a.hin = 1; a.win = rows; a.cin = k; a.hout = 1; a.wout = rows; a.cout = cout;
@@ -364,6 +390,7 @@ struct Exec {
     a.y2 = y2;
     a.aux = aux;
     a.gn = gn;
+    a.ln = ln;
     conv(a);
   }
   void groupnorm(RB x, int nb, int hw, int c, const NormW& n, bool silu, RB y, float* stats, RB x2 = RB(),
@@ -536,7 +563,7 @@ TransformerW load_transformer(Loader& L, const std::string& pre, int heads, cons
         f1bp[r] = f1b.data[src];
       }
   }
-  t.ff1 = L.linear_from(std::move(f1p), f1bp.data());
+  t.ff1 = L.linear_ln_from(std::move(f1p), f1bp.data(), b + "norm3", 1e-5f);   // norm3 folded
   t.ff2 = L.linear(b + "ff.net.2", true);
   t.c = t.proj_in.cout;
   return t;
@@ -754,8 +781,8 @@ class UNetPlan {
     RB r1 = buf(P, C), r2 = buf(P, C);
     float* sl2 = fbuf((long)P * 2);
     float* probs = fbuf((long)P * H);
-    RB l3 = buf(P, C);
     float* sl3 = fbuf((long)P * 2);
+    const dc_ln_fuse lnf3{t.ff1.csum, t.ff1.cbias, sl3};   // norm3 folded into ff.net.0.proj (unet.py ln_fuse)
     RB f8 = buf(P, 8 * C), gg = buf(P, 4 * C), r3 = buf(P, C), out = buf(P, C);
     TransformerW* tp = &t;
     Exec& ex = ex_;
@@ -768,9 +795,8 @@ class UNetPlan {
       DCK(dc_attn_fwd(qkv.p, qkv.ld, nb, T, H, o.p, o.ld, lse, ex.ws, ex.ws_bytes, ex.stream));
       ex.linear(o, tp->out.wf, tp->out.cin, P, C, r1, tp->out.bias, p);
       DCK(dc_crossattn_fwd(r1.p, r1.ld, P, C, H, tp->ln2.eps, tp->ln2.gamma, tp->ln2.beta, tp->tabs, tp->c0, r2.p,
-                           r2.ld, sl2, probs, ex.stream));
-      DCK(dc_layernorm_fwd(r2.p, r2.ld, P, C, tp->ln3.eps, tp->ln3.gamma, tp->ln3.beta, l3.p, l3.ld, sl3, ex.stream));
-      ex.linear(l3, tp->ff1.wf, tp->ff1.cin, P, 8 * C, f8, tp->ff1.bias, RB(), nullptr, 0, 1, gg);
+                           r2.ld, sl2, probs, sl3, tp->ln3.eps, ex.stream));
+      ex.linear(r2, tp->ff1.wf, tp->ff1.cin, P, 8 * C, f8, nullptr, RB(), nullptr, 0, 1, gg, RB(), nullptr, &lnf3);
       ex.linear(gg, tp->ff2.wf, tp->ff2.cin, P, C, r3, tp->ff2.bias, r2);
       ex.linear(r3, tp->proj_out.wf, tp->proj_out.cin, P, C, out, tp->proj_out.bias, x, nullptr, 0, 0, RB(), RB(),
                 gnf(out));
@@ -1035,7 +1061,7 @@ class UNetPlan {
     const int hh = d.i["hh"], ww = d.i["ww"], T = hh * ww, P = nb * T, C = t->c, H = t->heads;
     RB out = d.b["out"];
     RB dout = grad_of.at(out.p);
-    RB dr3 = buf(P, C), df = buf(P, 8 * C), dl3 = buf(P, C), dr2 = buf(P, C), dr1 = buf(P, C), dob = buf(P, C),
+    RB dr3 = buf(P, C), df = buf(P, 8 * C), dl3 = buf(P, C), dr1 = buf(P, C), dob = buf(P, C),
        dqkv = buf(P, 3 * C), dl1 = buf(P, C), dp = buf(P, C), dn0 = buf(P, C), dx = buf(P, C);
     float* delta = fbuf((long)nb * H * T);
     grad_of[x.p] = dx;
@@ -1050,10 +1076,9 @@ class UNetPlan {
       ex.linear(dout, t->proj_out.wd, t->proj_out.cout, P, C, dr3);
       ex.linear(dr3, t->ff2.wd, t->ff2.cout, P, 4 * C, df, nullptr, RB(), nullptr, 0, 2, RB(), f8);
       ex.linear(df, t->ff1.wd, t->ff1.cout, P, C, dl3);
-      DCK(dc_layernorm_bwd(r2.p, r2.ld, P, C, t->ln3.gamma, sl3, dl3.p, dl3.ld, dr2.p, dr2.ld, dr3.p, dr3.ld,
-                           ex.stream));
-      DCK(dc_crossattn_bwd(r1.p, r1.ld, P, C, H, t->ln2.gamma, t->tabs, sl2, probs, dr2.p, dr2.ld, dr1.p, dr1.ld,
-                           ex.stream));
+      // norm3 backward inside the cross-attention backward (dl3 = gamma3 dL/dLN3 through the folded weight)
+      DCK(dc_crossattn_bwd_ln(r1.p, r1.ld, P, C, H, t->ln2.gamma, t->tabs, sl2, probs, dl3.p, dl3.ld, r2.p, r2.ld, sl3,
+                              dr3.p, dr3.ld, dr1.p, dr1.ld, ex.stream));
       ex.linear(dr1, t->out.wd, t->out.cout, P, C, dob);
       DCK(dc_attn_bwd(qkv.p, qkv.ld, o.p, o.ld, dob.p, dob.ld, lse, nb, T, H, delta, dqkv.p, dqkv.ld, ex.ws,
                       ex.ws_bytes, ex.stream));

@@ -16,7 +16,7 @@ from pathlib import Path
 import torch
 
 from . import _lib
-from ._lib import ConvDesc, GnFuse, call
+from ._lib import ConvDesc, GnFuse, LnFuse, call
 
 BF16 = torch.bfloat16
 
@@ -142,9 +142,10 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
               cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
               c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
               y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None, geglu: int = 0,
-              y2=None, aux=None, rows=None, gn: GnFuse | None = None):
+              y2=None, aux=None, rows=None, gn: GnFuse | None = None, ln: LnFuse | None = None):
     """The dc_conv_desc of one conv_gemm call, its (algo, split) chosen (tuned table / nearest shape).
-    gn: fused GroupNorm statistics (include/dcamd.h dc_gn_fuse; the caller keeps it alive)."""
+    gn: fused GroupNorm statistics (include/dcamd.h dc_gn_fuse; the caller keeps it alive); ln: a LayerNorm of the
+    input rows folded in (dc_ln_fuse, ln_fuse below; the caller keeps it alive)."""
     d = ConvDesc()
     d.x = P(x)
     d.ldx = LD(x)
@@ -176,6 +177,8 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     d.ws_bytes = ctx.ws_bytes if splitk else 0
     if gn is not None:
         d.gn = C.pointer(gn)
+    if ln is not None:
+        d.ln = C.pointer(ln)
     if rows is not None:
         d.rows, d.nrows = rows[0].data_ptr(), int(rows[1])
         if algo is None:   # row counts vary per call: the library heuristic on nrows, not the tuned table
@@ -297,12 +300,20 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
 
 def linear(ctx: Ctx, x, w: torch.Tensor, rows: int, cout: int, y, bias=None, resid=None, rowbias=None,
            rowbias_ld: int = 0, act: int = 0, geglu: int = 0, y2=None, aux=None, algo: int | None = None,
-           nsplit: int | None = None, gn: GnFuse | None = None):
+           nsplit: int | None = None, gn: GnFuse | None = None, ln: LnFuse | None = None):
     """y[rows, cout] = x[rows, K] @ w[cout, K]^T (+ bias, + resid); geglu 1 / 2: the fused GEGLU
-    epilogues of include/dcamd.h (y2 = h * gelu(gate); aux = interleaved pre-activation)."""
+    epilogues of include/dcamd.h (y2 = h * gelu(gate); aux = interleaved pre-activation); ln: LayerNorm(x) as the
+    input (w the folded weight, dc_ln_fuse)."""
     return conv_gemm(ctx, x, w, nb=1, hin=1, win=rows, cin=w.shape[1], hout=1, wout=rows, cout=cout, kh=1, kw=1,
                      stride=1, pad=0, bias=bias, resid=resid, rowbias=rowbias, rowbias_ld=rowbias_ld, act=act, y=y,
-                     geglu=geglu, y2=y2, aux=aux, algo=algo, nsplit=nsplit, gn=gn)
+                     geglu=geglu, y2=y2, aux=aux, algo=algo, nsplit=nsplit, gn=gn, ln=ln)
+
+
+def ln_fuse(lin, stats) -> LnFuse:
+    """dc_ln_fuse of a weights.LnLinear with the input rows' (mean, rstd) in stats [rows][2] fp32."""
+    f = LnFuse()
+    f.csum, f.cbias, f.stats = lin.csum.data_ptr(), lin.cbias.data_ptr(), stats.data_ptr()
+    return f
 
 
 # ------------------------------------------------------------------------- norms
@@ -372,7 +383,8 @@ def layernorm(ctx: Ctx, x, rows, c, gamma, beta, eps, y, stats):
 
 
 def layernorm_bwd(ctx: Ctx, x, rows, c, gamma, stats, dy, dx, add=None):
-    call("dc_layernorm_bwd", P(x), LD(x), rows, c, gamma.data_ptr(), stats.data_ptr(), P(dy), LD(dy), P(dx), LD(dx),
+    """gamma None: dy is gamma * dL/dy already (the input-gradient of a folded weight, dc_ln_fuse)."""
+    call("dc_layernorm_bwd", P(x), LD(x), rows, c, P(gamma), stats.data_ptr(), P(dy), LD(dy), P(dx), LD(dx),
          P(add), LD(add), ctx.stream)
     return dx
 
@@ -398,10 +410,21 @@ def crossattn_tables(ctx: Ctx, U, D, heads, c) -> torch.Tensor:
     return tabs
 
 
-def crossattn_fwd(ctx: Ctx, x, rows, c, heads, eps, gamma, beta, tabs, c0, y, stats, probs):
+def crossattn_fwd(ctx: Ctx, x, rows, c, heads, eps, gamma, beta, tabs, c0, y, stats, probs, ystats=None,
+                  yeps=1e-5):
+    """ystats: [rows][2] (mean, rstd with yeps) of the output rows (norm3's statistics for dc_ln_fuse), or None."""
     call("dc_crossattn_fwd", P(x), LD(x), rows, c, heads, eps, gamma.data_ptr(), beta.data_ptr(), tabs.data_ptr(),
-         c0.data_ptr(), P(y), LD(y), stats.data_ptr(), probs.data_ptr(), ctx.stream)
+         c0.data_ptr(), P(y), LD(y), stats.data_ptr(), probs.data_ptr(), P(ystats), yeps, ctx.stream)
     return y
+
+
+def crossattn_bwd_ln(ctx: Ctx, x, rows, c, heads, gamma, tabs, stats, probs, dl, x3, stats3, add, dx):
+    """crossattn_bwd whose dy = LayerNorm3 backward of dl (gamma folded in, dc_ln_fuse) over x3, plus add, computed
+    in the same launch (dc_crossattn_bwd_ln)."""
+    call("dc_crossattn_bwd_ln", P(x), LD(x), rows, c, heads, gamma.data_ptr(), tabs.data_ptr(), stats.data_ptr(),
+         probs.data_ptr(), P(dl), LD(dl), P(x3), LD(x3), stats3.data_ptr(), P(add), LD(add), P(dx), LD(dx),
+         ctx.stream)
+    return dx
 
 
 def crossattn_bwd(ctx: Ctx, x, rows, c, heads, gamma, tabs, stats, probs, dy, dx):

@@ -16,7 +16,7 @@ import torch
 from . import ops
 from .config import UNetConfig
 from .ops import BF16, Ctx, Slice
-from .weights import Conv, Linear, Norm, fold_cross_attention, geglu_interleave, round_bf16
+from .weights import Conv, Linear, LnLinear, Norm, fold_cross_attention, geglu_interleave, round_bf16
 
 
 class ResnetW:
@@ -39,9 +39,17 @@ class ResnetW:
         self.temb_tables: dict = {}
 
 
+def ln_fuse_enabled() -> bool:
+    """LayerNorm norm3 folded into ff.net.0.proj (include/dcamd.h dc_ln_fuse: its statistics from the cross-attention
+    kernel that produces its input) and its backward into the cross-attention backward; DC_LN_FUSE=0: the separate
+    LayerNorm launches, for A/B runs and tests -- the native session always folds."""
+    return os.environ.get("DC_LN_FUSE", "1") != "0"
+
+
 class TransformerW:
     def __init__(self, sd, pre, dev, heads, ctx):
         self.heads = heads
+        self.ln_fused = ln_fuse_enabled()
         self.norm = Norm(sd[pre + "norm.weight"], sd[pre + "norm.bias"], dev, 1e-6)
         self.proj_in = Linear(sd[pre + "proj_in.weight"], sd[pre + "proj_in.bias"], dev)
         self.proj_out = Linear(sd[pre + "proj_out.weight"], sd[pre + "proj_out.bias"], dev)
@@ -57,7 +65,11 @@ class TransformerW:
         self.cross_tabs = None  # MFMA operand tables (ops.crossattn_tables), built with the first context
         # GEGLU projection with (h, gate) rows interleaved 8 + 8 for the fused epilogues (geglu_interleave)
         perm = geglu_interleave(sd[b + "ff.net.0.proj.weight"].shape[0])
-        self.ff1 = Linear(sd[b + "ff.net.0.proj.weight"][perm], sd[b + "ff.net.0.proj.bias"][perm], dev)
+        if self.ln_fused:   # norm3 folded into ff.net.0.proj
+            self.ff1 = LnLinear(sd[b + "ff.net.0.proj.weight"][perm], sd[b + "ff.net.0.proj.bias"][perm],
+                                sd[b + "norm3.weight"], sd[b + "norm3.bias"], 1e-5, dev)
+        else:
+            self.ff1 = Linear(sd[b + "ff.net.0.proj.weight"][perm], sd[b + "ff.net.0.proj.bias"][perm], dev)
         self.ff2 = Linear(sd[b + "ff.net.2.weight"], sd[b + "ff.net.2.bias"], dev)
         self.c = self.proj_in.cout
 
@@ -296,6 +308,7 @@ class UNetPlan:
         C, H = t.c, t.heads
         if t.cross_tabs is None:
             t.cross_tabs = ops.crossattn_tables(ctx, t.U, t.D, H, C)
+        fused = t.ln_fused
         n0 = self.buf(P, C)
         st0 = self.fbuf(nb, 32, 2)
         p = self.buf(P, C)
@@ -308,8 +321,10 @@ class UNetPlan:
         r2 = self.buf(P, C)
         sl2 = self.fbuf(P, 2)
         probs = self.fbuf(P, H)
-        l3 = self.buf(P, C)
+        l3 = None if fused else self.buf(P, C)
         sl3 = self.fbuf(P, 2)
+        lnf3 = ops.ln_fuse(t.ff1, sl3) if fused else None
+        self.saved.append(lnf3)
         f8 = self.buf(P, 8 * C)
         gg = self.buf(P, 4 * C)
         r3 = self.buf(P, C)
@@ -323,10 +338,14 @@ class UNetPlan:
             ops.linear(ctx, l1, t.qkv.wf, P, 3 * C, qkv)
             ops.attn_fwd(ctx, qkv, nb, T, H, o, lse)
             ops.linear(ctx, o, t.out.wf, P, C, r1, bias=t.out.bias, resid=p)
+            # (fused: with norm3's row statistics of its output r2)
             ops.crossattn_fwd(ctx, r1, P, C, H, t.ln2.eps, t.ln2.gamma, t.ln2.beta, t.cross_tabs, t.c0, r2, sl2,
-                              probs)
-            ops.layernorm(ctx, r2, P, C, t.ln3.gamma, t.ln3.beta, t.ln3.eps, l3, sl3)
-            ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias, geglu=1, y2=gg)   # + GEGLU
+                              probs, ystats=sl3 if fused else None, yeps=t.ln3.eps)
+            if fused:   # norm3 inside ff.net.0.proj (+ GEGLU)
+                ops.linear(ctx, r2, t.ff1.wf, P, 8 * C, f8, geglu=1, y2=gg, ln=lnf3)
+            else:
+                ops.layernorm(ctx, r2, P, C, t.ln3.gamma, t.ln3.beta, t.ln3.eps, l3, sl3)
+                ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias, geglu=1, y2=gg)   # + GEGLU
             ops.linear(ctx, gg, t.ff2.wf, P, C, r3, bias=t.ff2.bias, resid=r2)
             ops.linear(ctx, r3, t.proj_out.wf, P, C, out, bias=t.proj_out.bias, resid=x, gn=self._gnf(out))
 
@@ -534,7 +553,8 @@ class UNetPlan:
         dr3 = self.buf(P, C)
         df = self.buf(P, 8 * C)
         dl3 = self.buf(P, C)
-        dr2 = self.buf(P, C)
+        fused = t.ln_fused
+        dr2 = None if fused else self.buf(P, C)
         dr1 = self.buf(P, C)
         do = self.buf(P, C)
         dqkv = self.buf(P, 3 * C)
@@ -553,9 +573,12 @@ class UNetPlan:
         def b():
             ops.linear(ctx, dout, t.proj_out.wd, P, C, dr3)
             ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, df, geglu=2, aux=f8)   # + GEGLU backward
-            ops.linear(ctx, df, t.ff1.wd, P, C, dl3)
-            ops.layernorm_bwd(ctx, r2, P, C, t.ln3.gamma, sl3, dl3, dr2, add=dr3)
-            ops.crossattn_bwd(ctx, r1, P, C, H, t.ln2.gamma, t.cross_tabs, sl2, probs, dr2, dr1)
+            ops.linear(ctx, df, t.ff1.wd, P, C, dl3)   # (fused: gamma3 * dL/dLN3 through the folded weight)
+            if fused:   # norm3 backward inside the cross-attention backward
+                ops.crossattn_bwd_ln(ctx, r1, P, C, H, t.ln2.gamma, t.cross_tabs, sl2, probs, dl3, r2, sl3, dr3, dr1)
+            else:
+                ops.layernorm_bwd(ctx, r2, P, C, t.ln3.gamma, sl3, dl3, dr2, add=dr3)
+                ops.crossattn_bwd(ctx, r1, P, C, H, t.ln2.gamma, t.cross_tabs, sl2, probs, dr2, dr1)
             ops.linear(ctx, dr1, t.out.wd, P, C, do)
             ops.attn_bwd(ctx, qkv, o, do, lse, nb, T, H, delta, dqkv)
             ops.linear(ctx, dqkv, t.qkv.wd, P, C, dl1)

@@ -67,6 +67,32 @@ class Linear:
         self.wd = w.t().contiguous().to(device=device, dtype=BF16) if dgrad else None
 
 
+class LnLinear:
+    """A linear whose input is LayerNorm(x) (BasicTransformerBlock norm3 -> ff.net.0.proj), with the LayerNorm folded
+    in (include/dcamd.h dc_ln_fuse): wf = bf16(W diag(gamma)) and its input-gradient wd = wf^T (which yields
+    gamma * dL/dLN(x) for the LayerNorm backward), csum[n] = sum_k wf[n][k], cbias[n] = W[n] . beta + bias[n].
+    Computed by the library's dc_fold_layernorm (host code shared with the native session)."""
+
+    def __init__(self, w, b, norm_w, norm_b, eps, device):
+        from . import _lib
+
+        w = round_bf16(w).contiguous()
+        self.cout, self.cin = w.shape
+        self.eps = eps
+        g = round_bf16(norm_w).contiguous()
+        be = round_bf16(norm_b).contiguous()
+        bias = b.float().to(BF16).float().contiguous() if b is not None else None
+        wf = torch.empty(self.cout, self.cin, dtype=BF16)
+        csum = torch.empty(self.cout, dtype=torch.float32)
+        cbias = torch.empty(self.cout, dtype=torch.float32)
+        _lib.call("dc_fold_layernorm", w.data_ptr(), self.cout, self.cin, g.data_ptr(), be.data_ptr(),
+                  bias.data_ptr() if bias is not None else None, wf.data_ptr(), csum.data_ptr(), cbias.data_ptr())
+        self.wf = wf.to(device)
+        self.wd = wf.t().contiguous().to(device)
+        self.csum = csum.to(device)
+        self.cbias = cbias.to(device)
+
+
 def geglu_interleave(n_out: int) -> torch.Tensor:
     """Row order of the GEGLU projection (ff.net.0.proj, [2 * inner][C]) for the fused epilogue of
     dc_conv_gemm (geglu = 1 / 2): blocks of 8 h rows then the 8 matching gate rows."""

@@ -65,6 +65,24 @@ typedef struct dc_gn_fuse {
   int silu;
 } dc_gn_fuse;
 long long dc_gn_acc_bytes(int nb, int groups);
+/* LayerNorm of the input rows folded into a linear (BasicTransformerBlock norm3 -> ff.net.0.proj,
+ * marigold_dc.py:460-465 through diffusers): with W' = bf16(W diag(gamma)) as the call's weight, csum[n] =
+ * sum_k W'[n][k] and cbias[n] = sum_k W[n][k] beta[k] + bias[n] (dc_fold_layernorm), and the input rows' (mean, rstd)
+ * in stats[rows][2] (dc_crossattn_fwd's ystats: the producer of norm3's input holds whole rows), the epilogue stores
+ *   y = rstd (x . W'^T - mean csum) + cbias  =  LayerNorm(x) . W^T + bias   (up to rounding),
+ * so the normalised rows are never written.  The input-gradient of the folded weight (W'^T) yields gamma * dL/dLN(x)
+ * (dc_crossattn_bwd_ln / dc_layernorm_bwd with gamma NULL take it from there).
+ * Contract: a linear (1x1, stride 1, pad 0, mode 0) with cin == ktot, no second source, no row list, no GroupNorm
+ * fusion, bias NULL (cbias replaces it), geglu 0 or 1; the im2col tile variants (another choice runs the heuristic). */
+typedef struct dc_ln_fuse {
+  const float* csum;
+  const float* cbias;
+  const float* stats;
+} dc_ln_fuse;
+/* the folded weight and its column constants, on the host (the Python host and the native session share it):
+ * w, gamma, beta fp32 (bf16-exact values), bias fp32 or NULL; wf bf16 [cout][k] out; csum, cbias fp32 [cout] out */
+int dc_fold_layernorm(const float* w, int cout, int k, const float* gamma, const float* beta, const float* bias,
+                      void* wf, float* csum, float* cbias);
 /* 1 where the fused statistics pay for a GroupNorm of hw pixels x c channels (forward / backward): not where the
  * single-launch GroupNorm (one block per group, levels 2-3 of the UNet) runs it.  Both hosts plan with it. */
 int dc_gn_fuse_pays(int hw, int c, int groups, int backward);
@@ -114,6 +132,8 @@ typedef struct dc_conv_desc {
   int nrows;
   /* optional fused GroupNorm statistics (above; NULL: none).  Needs cout % 8 == 0, no row list, no GEGLU. */
   const dc_gn_fuse* gn;
+  /* optional LayerNorm of the input rows folded in (dc_ln_fuse above; NULL: none) */
+  const dc_ln_fuse* ln;
 } dc_conv_desc;
 
 int dc_conv_num_algos(void);
@@ -143,6 +163,7 @@ int dc_groupnorm_bwd_acc(const void* x, int ldx, const void* x2, int ldx2, int c
                          void* stream);
 int dc_layernorm_fwd(const void* x, int ldx, long long rows, int c, float eps, const float* gamma, const float* beta,
                      void* y, int ldy, float* stats, void* stream);
+/* gamma NULL: dy is already gamma * dL/dy (the input-gradient of a dc_ln_fuse folded weight) */
 int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, const float* gamma, const float* stats,
                      const void* dy, int lddy, void* dx, int lddx, const void* add, int ldadd, void* stream);
 
@@ -163,12 +184,20 @@ int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, const void* dou
  * for the backward. */
 long long dc_crossattn_tables_bytes(int heads, int c);
 int dc_crossattn_prepare(const float* U, const float* D, int heads, int c, void* tabs, void* stream);
+/* ystats: NULL, or [rows][2] (mean, rstd with eps yeps) of the output rows y (norm3's statistics, dc_ln_fuse) */
 int dc_crossattn_fwd(const void* x, int ldx, long long rows, int c, int heads, float eps, const float* gamma,
                      const float* beta, const void* tabs, const float* c0, void* y, int ldy, float* stats,
-                     float* probs, void* stream);
+                     float* probs, float* ystats, float yeps, void* stream);
 int dc_crossattn_bwd(const void* x, int ldx, long long rows, int c, int heads, const float* gamma, const void* tabs,
                      const float* stats, const float* probs, const void* dy, int lddy, void* dx, int lddx,
                      void* stream);
+/* the same with its dy computed in the launch: dy = LayerNorm backward (norm3, BasicTransformerBlock) of dl, which is
+ * gamma3 * dL/dLN3(x3) (the input-gradient of the folded ff.net.0.proj, dc_ln_fuse), over x3 with stats3 [rows][2]
+ * (mean, rstd), plus add (the residual gradient): the arithmetic of dc_layernorm_bwd with gamma NULL, so the result
+ * equals dc_layernorm_bwd followed by dc_crossattn_bwd bit for bit. */
+int dc_crossattn_bwd_ln(const void* x, int ldx, long long rows, int c, int heads, const float* gamma, const void* tabs,
+                        const float* stats, const float* probs, const void* dl, int lddl, const void* x3, int ldx3,
+                        const float* stats3, const void* add, int ldadd, void* dx, int lddx, void* stream);
 
 /* ---------------------------------------------------------------- elementwise
  * GEGLU (FeedForward.net[0]), nearest-upsample adjoint (Upsample2D / TAESD Upsample backward),

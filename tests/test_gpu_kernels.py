@@ -319,6 +319,91 @@ def test_layernorm_fwd_bwd(ctx, c):
     assert rel(dx, x.grad) < 2e-2
 
 
+@pytest.mark.parametrize("c,n,geglu", [(320, 960, 0), (640, 1920, 0), (1280, 3840, 0), (320, 2560, 1),
+                                        (1280, 10240, 1)])
+@pytest.mark.parametrize("algo,nsplit", [(13, 1), (12, 1), (3, 1), (37, 1), (18, 1), (13, 3), (12, -1)])
+def test_linear_ln_fused(ctx, c, n, geglu, algo, nsplit):
+    """LayerNorm folded into the consuming linear (dc_ln_fuse: the rows' (mean, rstd) given, the normalisation
+    applied in the epilogue after split-K / stream-K sums) against torch: bf16(LayerNorm(x)) @ W^T + bias in fp32.
+    Rows with a large common offset check that the mean is subtracted after the product, on the folded weight's
+    own column sums."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import LnLinear
+    rows = 333
+    x = (rnd(rows, c, seed=70) * 2 + 3 * rnd(rows, 1, seed=71)).to(torch.bfloat16).float()
+    x[5] += 40.0   # |mean| >> std on one row
+    x = x.to(torch.bfloat16).float()
+    gamma = (1 + 0.2 * rnd(c, seed=72)).to(torch.bfloat16).float()
+    beta = (0.2 * rnd(c, seed=73)).to(torch.bfloat16).float()
+    w = rnd(n, c, scale=1 / math.sqrt(c), seed=74)
+    b = 0.1 * rnd(n, seed=75)
+    lin = LnLinear(w.cpu(), b.cpu(), gamma.cpu(), beta.cpu(), 1e-5, dev)
+    l = F.layer_norm(x, (c,), gamma, beta, 1e-5).to(torch.bfloat16).float()
+    ref = l @ w.to(torch.bfloat16).float().t() + b.to(torch.bfloat16).float()
+    st = torch.stack([x.mean(1), torch.rsqrt(x.var(1, unbiased=False) + 1e-5)], 1).contiguous()
+    y = torch.zeros(rows, n, dtype=torch.bfloat16, device=dev)
+    y2 = torch.zeros(rows, n // 2, dtype=torch.bfloat16, device=dev) if geglu else None
+    f = ops.ln_fuse(lin, st)
+    ops.linear(ctx, x.to(torch.bfloat16), lin.wf, rows, n, y, geglu=geglu, y2=y2, ln=f, algo=algo, nsplit=nsplit)
+    torch.cuda.synchronize()
+    assert rel(y, ref) < 1e-2
+    if geglu:
+        hh = ref.view(rows, n // 16, 2, 8)[:, :, 0].reshape(rows, n // 2)
+        gt = ref.view(rows, n // 16, 2, 8)[:, :, 1].reshape(rows, n // 2)
+        assert rel(y2, hh * F.gelu(gt)) < 2e-2
+    # the input-gradient through the folded weight is gamma * dL/dLN(x); with the LayerNorm backward (gamma NULL)
+    # it gives dL/dx
+    if not geglu and algo == 13 and nsplit == 1:
+        xr = x.clone().requires_grad_(True)
+        out = F.layer_norm(xr, (c,), gamma, beta, 1e-5) @ w.to(torch.bfloat16).float().t()
+        gy = rnd(rows, n, seed=76)
+        out.backward(gy)
+        dl = torch.empty(rows, c, dtype=torch.bfloat16, device=dev)
+        ops.linear(ctx, gy.to(torch.bfloat16), lin.wd, rows, c, dl)
+        dx = torch.empty(rows, c, dtype=torch.bfloat16, device=dev)
+        ops.layernorm_bwd(ctx, x.to(torch.bfloat16), rows, c, None, st, dl, dx)
+        torch.cuda.synchronize()
+        assert rel(dx, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("C,heads", [(320, 5), (640, 10), (1280, 20)])
+def test_cross_bwd_ln3_fused(ctx, C, heads):
+    """dc_crossattn_bwd_ln (norm3 backward computed in the cross-attention backward's launch) equals
+    dc_layernorm_bwd (gamma folded) followed by dc_crossattn_bwd bit for bit, ragged row count included."""
+    from depth_completion_amd import ops
+    rows = 333
+    g = torch.Generator().manual_seed(77)
+    U = (torch.randn(heads, C, generator=g) / math.sqrt(C)).to(dev)
+    D = (torch.randn(heads, C, generator=g) / math.sqrt(C)).to(dev)
+    gamma2 = (1 + 0.1 * torch.randn(C, generator=g)).to(torch.bfloat16).float().to(dev)
+    beta2 = (0.1 * torch.randn(C, generator=g)).to(torch.bfloat16).float().to(dev)
+    c0 = (0.1 * torch.randn(C, generator=g)).to(dev)
+    r1 = rnd(rows, C, scale=2, seed=78).to(torch.bfloat16)
+    tabs = ops.crossattn_tables(ctx, U, D, heads, C)
+    r2 = torch.empty(rows, C, dtype=torch.bfloat16, device=dev)
+    sl2 = torch.empty(rows, 2, device=dev)
+    pr = torch.empty(rows, heads, device=dev)
+    sl3 = torch.zeros(rows, 2, device=dev)
+    ops.crossattn_fwd(ctx, r1, rows, C, heads, 1e-5, gamma2, beta2, tabs, c0, r2, sl2, pr, ystats=sl3, yeps=1e-5)
+    # norm3's statistics of the output rows (dc_crossattn_fwd ystats) against torch on the stored bf16 rows
+    r2f = r2.float()
+    torch.testing.assert_close(sl3[:, 0], r2f.mean(1), rtol=0, atol=1e-5)
+    torch.testing.assert_close(sl3[:, 1], torch.rsqrt(r2f.var(1, unbiased=False) + 1e-5), rtol=1e-5, atol=0)
+    r2b = torch.empty_like(r2)
+    ops.crossattn_fwd(ctx, r1, rows, C, heads, 1e-5, gamma2, beta2, tabs, c0, r2b, sl2, pr)
+    assert torch.equal(r2, r2b)   # the statistics pass changes no output
+    dl3 = rnd(rows, C, seed=79).to(torch.bfloat16)
+    dr3 = rnd(rows, C, seed=80).to(torch.bfloat16)
+    dr2 = torch.empty(rows, C, dtype=torch.bfloat16, device=dev)
+    ops.layernorm_bwd(ctx, r2, rows, C, None, sl3, dl3, dr2, add=dr3)
+    dx_a = torch.empty(rows, C, dtype=torch.bfloat16, device=dev)
+    ops.crossattn_bwd(ctx, r1, rows, C, heads, gamma2, tabs, sl2, pr, dr2, dx_a)
+    dx_b = torch.zeros(rows, C, dtype=torch.bfloat16, device=dev)
+    ops.crossattn_bwd_ln(ctx, r1, rows, C, heads, gamma2, tabs, sl2, pr, dl3, r2, sl3, dr3, dx_b)
+    torch.cuda.synchronize()
+    assert torch.equal(dx_a, dx_b)
+
+
 # ----------------------------------------------------------------------------- attention
 # the last shape launches >= 1024 blocks (no key split), the others the 2-way key-split kernels
 @pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (2, 300, 2), (1, 1000, 5), (1, 108, 20), (16, 1000, 8)])

@@ -61,7 +61,10 @@ def test_unet_plan_sequence(rec, which, h, w):
     nb = len(rec.calls) - nf
     # 22 resnets, 16 transformers in the SD topology
     assert rec.calls.count("dc_attn_fwd") == 16 and rec.calls.count("dc_attn_bwd") == 16
-    assert rec.calls.count("dc_crossattn_fwd") == 16 and rec.calls.count("dc_crossattn_bwd") == 16
+    # norm3 folded into ff.net.0.proj (dc_ln_fuse) and its backward into the cross-attention backward: norm1's
+    # forward and backward remain
+    assert rec.calls.count("dc_crossattn_fwd") == 16 and rec.calls.count("dc_crossattn_bwd_ln") == 16
+    assert rec.calls.count("dc_layernorm_fwd") == 16 and rec.calls.count("dc_layernorm_bwd") == 16
     assert nf > 100 and nb > 100
 
 

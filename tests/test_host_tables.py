@@ -91,6 +91,31 @@ def test_fold_cross_attention_matches_attn2_on_two_tokens():
     torch.testing.assert_close(folded, ref, rtol=1e-6, atol=1e-6)
 
 
+def test_fold_layernorm_matches_definition():
+    """dc_fold_layernorm (weights.LnLinear, shared with the native session): wf = bf16(W diag(gamma)),
+    csum = row sums of wf, cbias = W . beta + bias; LayerNorm(x) @ W^T + bias == rstd (x @ wf^T - mean csum) + cbias
+    in exact arithmetic, up to bf16 rounding of the folded weight."""
+    from depth_completion_amd.weights import LnLinear, round_bf16
+    g = torch.Generator().manual_seed(5)
+    n, k = 48, 64
+    w = torch.randn(n, k, generator=g)
+    b = torch.randn(n, generator=g) * 0.1
+    gam = 1 + 0.2 * torch.randn(k, generator=g)
+    bet = 0.2 * torch.randn(k, generator=g)
+    lin = LnLinear(w, b, gam, bet, 1e-5, "cpu")
+    wr, gr, br, bb = round_bf16(w), round_bf16(gam), round_bf16(bet), round_bf16(b)
+    assert torch.equal(lin.wf, (wr * gr).to(torch.bfloat16))
+    assert torch.equal(lin.wd, lin.wf.t())
+    torch.testing.assert_close(lin.csum.double(), lin.wf.double().sum(1), rtol=1e-7, atol=1e-9)
+    torch.testing.assert_close(lin.cbias.double(), wr.double() @ br.double() + bb.double(), rtol=1e-7, atol=1e-9)
+    x = torch.randn(5, k, generator=g) * 3 + 2
+    mu = x.mean(1, keepdim=True)
+    rs = torch.rsqrt(x.var(1, unbiased=False, keepdim=True) + 1e-5)
+    ref = torch.nn.functional.layer_norm(x, (k,), gr, br, 1e-5) @ wr.t() + bb
+    got = rs * (x @ lin.wf.float().t() - mu * lin.csum) + lin.cbias
+    assert float((got - ref).norm() / ref.norm()) < 1e-2
+
+
 def test_clip_empty_prompt_matches_transformers():
     transformers = pytest.importorskip("transformers")
     cfg = transformers.CLIPTextConfig(vocab_size=49408, hidden_size=64, intermediate_size=128, num_hidden_layers=2,
