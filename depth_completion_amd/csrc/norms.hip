@@ -324,10 +324,12 @@ __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* 
   const float* abn = ab + (long)n * s.groups * 2;
   const int rbeg = blockIdx.x * s.apply_rows, rend = min(s.hw, rbeg + s.apply_rows), row0 = rbeg + r0;
   const bool pf = s.pf && (part || acc) && r0 < s.R && row0 < rend;  // as gn_apply_kernel
-  float f0[8], d0[8];
+  float f0[8], d0[8], e10[8], e20[8];   // (the first row's residual inputs too: no second round trip after the fold)
   if (pf) {
     gn_load8(s, n, row0, cg * 8, f0);
     load8(dy + ((long)n * s.hw + row0) * lddy + cg * 8, d0);
+    if (add1) load8(add1 + ((long)n * s.hw + row0) * ldadd1 + cg * 8, e10);
+    if (add2) load8(add2 + ((long)n * s.hw + row0) * ldadd2 + cg * 8, e20);
   }
   if (acc) {
     float* grp = reinterpret_cast<float*>(gsh + 2 * s.groups);
@@ -375,15 +377,26 @@ __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* 
       }
       out[k] = rs[k] * (dd * ga[k] - ma[k] - xhat * mb[k]);
     }
+    const bool first = pf && row == row0;
     if (add1) {
       float e[8];
-      load8(add1 + pix * ldadd1 + cg * 8, e);
+      if (first) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e[k] = e10[k];
+      } else {
+        load8(add1 + pix * ldadd1 + cg * 8, e);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) out[k] = (float)(bf16)out[k] + e[k];
     }
     if (add2) {
       float e[8];
-      load8(add2 + pix * ldadd2 + cg * 8, e);
+      if (first) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) e[k] = e20[k];
+      } else {
+        load8(add2 + pix * ldadd2 + cg * 8, e);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) out[k] = (float)(bf16)out[k] + e[k];
     }
@@ -547,6 +560,21 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
     }
     return dd * ga[i];
   };
+  // the residual inputs of the thread's first kPA rows go out with the pass-1 loads (no second round trip after the
+  // block reduction)
+  constexpr int kPA = 4;
+  bfvec<VEC> pa1[kPA], pa2[kPA];
+  const long pix0 = (long)n * s.hw;
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < kPA; ++j) {
+      const int row = r0 + j * RP;
+      if (row < s.hw) {
+        if (add1) pa1[j] = *reinterpret_cast<const bfvec<VEC>*>(add1 + (pix0 + row) * ldadd1 + ch);
+        if (add2) pa2[j] = *reinterpret_cast<const bfvec<VEC>*>(add2 + (pix0 + row) * ldadd2 + ch);
+      }
+    }
+  }
   float sa = 0.0f, sb = 0.0f;
   if (act) {
     for (int r = r0; r < s.hw; r += RP * U) {
@@ -580,8 +608,7 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
   const float ma = (float)(ta / cnt), mb = (float)(tb / cnt);
   if (!act) return;
   bf16* dst = dx + (long)n * s.hw * lddx + ch;
-  const long pix0 = (long)n * s.hw;
-  for (int row = r0; row < s.hw; row += RP) {
+  for (int row = r0, j = 0; row < s.hw; row += RP, ++j) {
     const bfvec<VEC> rx = sx[row * vpr + v], rd = sd[row * vpr + v];
     float out[VEC];
 #pragma unroll
@@ -591,12 +618,26 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
       out[i] = rs * (gd - ma - xh * mb);
     }
     if (add1) {
-      const bfvec<VEC> e = *reinterpret_cast<const bfvec<VEC>*>(add1 + (pix0 + row) * ldadd1 + ch);
+      bfvec<VEC> e;
+      if (j < kPA) {
+#pragma unroll
+        for (int q = 0; q < kPA; ++q)
+          if (q == j) e = pa1[q];   // (static register indexing)
+      } else {
+        e = *reinterpret_cast<const bfvec<VEC>*>(add1 + (pix0 + row) * ldadd1 + ch);
+      }
 #pragma unroll
       for (int i = 0; i < VEC; ++i) out[i] = (float)(bf16)out[i] + (float)e[i];
     }
     if (add2) {
-      const bfvec<VEC> e = *reinterpret_cast<const bfvec<VEC>*>(add2 + (pix0 + row) * ldadd2 + ch);
+      bfvec<VEC> e;
+      if (j < kPA) {
+#pragma unroll
+        for (int q = 0; q < kPA; ++q)
+          if (q == j) e = pa2[q];
+      } else {
+        e = *reinterpret_cast<const bfvec<VEC>*>(add2 + (pix0 + row) * ldadd2 + ch);
+      }
 #pragma unroll
       for (int i = 0; i < VEC; ++i) out[i] = (float)(bf16)out[i] + (float)e[i];
     }
@@ -885,7 +926,7 @@ __global__ void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const fl
   if (row >= rows) return;
   const int nv = c >> 3;
   const float mu = stats[row * 2], rs = stats[row * 2 + 1];
-  float xh[MAXV][8], g[MAXV][8];
+  float xh[MAXV][8], g[MAXV][8], ad[MAXV][8];
   float sa = 0.0f, sb = 0.0f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
@@ -894,6 +935,7 @@ __global__ void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const fl
       float f[8], d[8];
       load8(x + row * ldx + vi * 8, f);
       load8(dy + row * lddy + vi * 8, d);
+      if (add) load8(add + row * ldadd + vi * 8, ad[k]);   // with the other loads: one round trip
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         xh[k][i] = (f[i] - mu) * rs;
@@ -912,10 +954,8 @@ __global__ void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const fl
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = rs * (g[k][i] - ma - xh[k][i] * mb);
       if (add) {
-        float e[8];
-        load8(add + row * ldadd + vi * 8, e);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)o[i] + e[i];
+        for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)o[i] + ad[k][i];
       }
       store8(dx + row * lddx + vi * 8, o);
     }
