@@ -80,7 +80,8 @@ struct ConvGemmParams {
   const int* rows;      // optional: GEMM row m computes output pixel rows[m] (sorted), nrows of them
   long nrows;
   int diag;             // kernel diagnostics (env DC_HALO_DIAG, experiments only): halo 1 no LDS-DMA, 2 no MFMA
-                        // / fragment reads, 4 no barrier; 8 no GroupNorm-statistics accumulator adds
+                        // / fragment reads, 4 no barrier; 8 no GroupNorm-statistics accumulator adds; 256 epilogue
+                        // operands loaded in the epilogue (the round-3 placement, A/B)
   int nmajor;           // tile order within an XCD's range: 0 M-major (row tiles share A), 1 N-major (column
                         // tiles share W; opt-in, DC_GEMM_ORDER=2)
   // multiply-shift division by hout * wout, wout and hout (fast_div): the pixel -> (frame, y, x) split of
@@ -207,6 +208,78 @@ __device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, 
   } else {
     for (int i = 0; i < cnt; ++i) out[i] = (bf16)v[i];
   }
+}
+
+// ---- epilogue operands loaded ahead.  Loaded where epilogue_store uses them, the column bias, then the row-bias /
+// residual / mask vectors are each a dependent memory round trip at the end of the tile (after the staging barrier);
+// loaded at kernel start (or before the staging barrier where the registers are scarce) they land under the main
+// loop.  RMAX = the lane's 16-B output rows (lane + 64 r of the wave's WM x WN / 8 row-vectors; GPR divides 64, so a
+// lane keeps one 8-channel column group).
+template <int NJ, int RMAX>
+struct EpiPre {
+  float cv[NJ];        // per-column bias (GNM 3: csum)
+  float cv2[NJ];       // GNM 3: cbias
+  bf16x8 rb;           // row bias (per-step table row) of the lane's 8 columns
+  bf16x8 res[RMAX], msk[RMAX];
+  long mrow[RMAX];     // output pixel of each row-vector (-1: none)
+};
+template <int GNM, int NJ, int RMAX>
+__device__ __forceinline__ void epi_cols(const ConvGemmParams& p, int c0, EpiPre<NJ, RMAX>& e) {
+  // c0 = the lane's first column (n0 + wn WN + lane % 16); column j = c0 + 16 j
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = c0 + j * 16;
+    if constexpr (GNM == 3) {
+      e.cv[j] = c < p.cout ? p.ln_csum[c] : 0.0f;
+      e.cv2[j] = c < p.cout ? p.ln_cbias[c] : 0.0f;
+    } else {
+      e.cv[j] = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+    }
+  }
+}
+template <int WM, int GPR, int NJ, int RMAX>
+__device__ __forceinline__ void epi_rows(const ConvGemmParams& p, long mw, int c, long M, int lane,
+                                         EpiPre<NJ, RMAX>& e) {
+  // mw = the wave's first output row, c = the lane's 8-channel group (n0 + wn WN + (lane % GPR) 8)
+  const bool full = c + 8 <= p.cout;
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) {
+    const int g = lane + 64 * r;
+    const long m = mw + g / GPR;
+    e.mrow[r] = (g < WM * GPR && m < M && c < p.cout) ? conv_pix(p, m) : -1;
+    if (e.mrow[r] >= 0 && full) {
+      if (p.resid) e.res[r] = *reinterpret_cast<const bf16x8*>(p.resid + e.mrow[r] * p.ldr + c);
+      if (p.mask) e.msk[r] = *reinterpret_cast<const bf16x8*>(p.mask + e.mrow[r] * p.ldmask + c);
+    }
+  }
+  if (p.rowbias && full) e.rb = *reinterpret_cast<const bf16x8*>(p.rowbias + (long)(*p.rowbias_idx) * p.rowbias_ld + c);
+}
+// epilogue_store with the row-vector's preloaded operands (partial vectors, cout % 8 != 0, load as before)
+template <int NJ, int RMAX>
+__device__ __forceinline__ void epilogue_store_pre(const ConvGemmParams& p, const EpiPre<NJ, RMAX>& e, int r, int c,
+                                                   float* v) {
+  const long m = e.mrow[r];
+  if (c + 8 > p.cout) {
+    epilogue_store(p, m, c, v, false);
+    return;
+  }
+  if (p.rowbias) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)(bf16)v[i] + (float)e.rb[i];
+  }
+  if (p.resid) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)(bf16)v[i] + (float)e.res[r][i];
+  }
+  if (p.act == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = fmaxf(v[i], 0.0f);
+  }
+  if (p.mask) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)e.msk[r][i] > 0.0f ? v[i] : 0.0f;
+  }
+  store8(p.y + m * p.ldy + c, v);
 }
 
 // ---- GroupNorm statistics fused into the epilogue (include/dcamd.h dc_gn_fuse; the host guarantees cout % 8 == 0,
@@ -777,16 +850,39 @@ __device__ __forceinline__ bool tile_handoff(const ConvGemmParams& p, char* smem
   return tile_handoff_g<BM / 32, BN / 32>(p, smem, tile, my_slot, narrive, slot_of, acc);
 }
 
+// the preloaded epilogue operands of a BM x BN tile (4 waves, 2 x 2)
+template <int BM, int BN>
+struct TileEpi {
+  static constexpr int WM = BM / 2, WN = BN / 2, NJ = WN / 16, GPR = WN / 8;
+  static constexpr int RMAX = (WM * GPR + 63) / 64;
+  // a lane keeps one 8-channel column group only where GPR divides 64 (not the 320-wide tiles): else no row preload
+  static constexpr bool kRows = 64 % GPR == 0;
+  static constexpr bool kEarly = kRows && RMAX <= 4;   // row operands loaded at kernel start (else before the staging)
+  using Pre = EpiPre<NJ, RMAX>;
+};
+template <int BM, int BN, int GNM>
+__device__ __forceinline__ void tile_epi_load(const ConvGemmParams& p, long m0, int n0, bool rows,
+                                              typename TileEpi<BM, BN>::Pre& e) {
+  using TE = TileEpi<BM, BN>;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  if (!rows) epi_cols<GNM>(p, n0 + wn * TE::WN + (lane & 15), e);
+  if (rows && TE::kRows && GNM != 1 && GNM != 2 && !p.geglu)
+    epi_rows<TE::WM, TE::GPR>(p, m0 + wm * TE::WM, n0 + wn * TE::WN + (lane % TE::GPR) * 8, conv_rows(p), lane, e);
+}
+
 // epilogue: bias in fp32, round to bf16 into a per-wave LDS tile, then 16-B coalesced rows
 template <int BM, int BN, int GNM, int LDSB>
 __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* smem, long m0, int n0,
-                                              const f32x4 (&acc)[BM / 32][BN / 32]) {
+                                              const f32x4 (&acc)[BM / 32][BN / 32], typename TileEpi<BM, BN>::Pre& pre) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int MI = WM / 16, NJ = WN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const long M = conv_rows(p);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+  if (!TileEpi<BM, BN>::kEarly || (p.diag & 256)) tile_epi_load<BM, BN, GNM>(p, m0, n0, true, pre);
+  if (p.diag & 256) tile_epi_load<BM, BN, GNM>(p, m0, n0, false, pre);   // A/B: the late (round-3) placement
   __syncthreads();  // every wave is done reading the ring
   constexpr int LDE = WN + 8;
   bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
@@ -805,9 +901,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
       }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int c = n0 + wn * WN + j * 16 + col_l;
-      const float cs = c < p.cout ? p.ln_csum[c] : 0.0f;
-      const float cb = c < p.cout ? p.ln_cbias[c] : 0.0f;
+      const float cs = pre.cv[j], cb = pre.cv2[j];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -817,8 +911,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
   } else {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int c = n0 + wn * WN + j * 16 + col_l;
-      const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+      const float bv = pre.cv[j];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -886,15 +979,28 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
     return;
   }
   if (p.diag & 64) return;   // experiments only: no epilogue stores
+  if constexpr (!TileEpi<BM, BN>::kRows) {
 #pragma unroll 4
-  for (int g = lane; g < WM * GPR; g += 64) {
-    const int row = g / GPR, cg = g - (g / GPR) * GPR;
-    const long m = m0 + wm * WM + row;
-    const int c = n0 + wn * WN + cg * 8;
-    if (m >= M || c >= p.cout) continue;
+    for (int g = lane; g < WM * GPR; g += 64) {
+      const int row = g / GPR, cg = g - (g / GPR) * GPR;
+      const long m = m0 + wm * WM + row;
+      const int c = n0 + wn * WN + cg * 8;
+      if (m >= M || c >= p.cout) continue;
+      float v[8];
+      load8(es + row * LDE + cg * 8, v);
+      epilogue_store(p, conv_pix(p, m), c, v, false);
+    }
+    return;
+  }
+  constexpr int RMAX = TileEpi<BM, BN>::RMAX;
+  const int cg = lane % GPR, c = n0 + wn * WN + cg * 8;
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) {
+    if (pre.mrow[r] < 0) continue;
+    const int row = (lane + 64 * r) / GPR;
     float v[8];
     load8(es + row * LDE + cg * 8, v);
-    epilogue_store(p, conv_pix(p, m), c, v, false);
+    epilogue_store_pre(p, pre, r, c, v);
   }
 }
 
@@ -913,7 +1019,7 @@ template <int BM, int BN, int BK, int S, bool SMALLC, bool SK, int GNM>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[Cfg<BM, BN, BK, S>::LDS];
   f32x4 acc[BM / 32][BN / 32];
-  if (p.diag & 128) return;   // experiments only: the launch and dispatch alone (tools/launch_floor.py)
+  typename TileEpi<BM, BN>::Pre pre;
   const int tiles_n = (p.cout + BN - 1) / BN;
   const int nk = p.ktot / BK;
 
@@ -943,12 +1049,17 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     const int n0 = tn * BN;
     const int kc_begin = split * p.kps;
     const int kc_end = min(nk, kc_begin + p.kps);
+    // the epilogue's column operands (and, where registers allow, its row operands) in flight under the main loop
+    if (!(p.diag & 256)) {
+      tile_epi_load<BM, BN, GNM>(p, m0, n0, false, pre);
+      if (TileEpi<BM, BN>::kEarly) tile_epi_load<BM, BN, GNM>(p, m0, n0, true, pre);
+    }
     tile_pass<BM, BN, BK, S, SMALLC>(p, smem, m0, n0, kc_begin, kc_end, acc);
     if (p.splits > 1 &&
         !tile_handoff<BM, BN>(p, smem, lb, split * tiles + lb, p.splits, [&](int sp) { return sp * tiles + lb; },
                               acc))
       return;
-    tile_epilogue<BM, BN, GNM, Cfg<BM, BN, BK, S>::LDS>(p, smem, m0, n0, acc);
+    tile_epilogue<BM, BN, GNM, Cfg<BM, BN, BK, S>::LDS>(p, smem, m0, n0, acc, pre);
   } else {
   // stream-K: the tiles x nk k-chunk iterations are dealt out as G equal contiguous ranges (logical
   // block b gets [b U / G, (b + 1) U / G)), so every block does the same MFMA work whatever the tile
@@ -969,6 +1080,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     tile_coords(p, tile, p.splits / tiles_n, tiles_n, tm, tn);
     const long m0 = (long)tm * BM;
     const int n0 = tn * BN;
+    if (!(p.diag & 256)) {
+      tile_epi_load<BM, BN, GNM>(p, m0, n0, false, pre);
+      if (TileEpi<BM, BN>::kEarly) tile_epi_load<BM, BN, GNM>(p, m0, n0, true, pre);
+    }
     tile_pass<BM, BN, BK, S, SMALLC>(p, smem, m0, n0, kb, ke, acc);
     bool mine = true;
     if (kb != 0 || ke != nk) {
@@ -979,7 +1094,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
           p, smem, tile, slot, bl - bf + 1,
           [&](int i) { const int bb = bf + i; return ((long)bb * U / G >= t0) ? 2 * bb : 2 * bb + 1; }, acc);
     }
-    if (mine) tile_epilogue<BM, BN, GNM, Cfg<BM, BN, BK, S>::LDS>(p, smem, m0, n0, acc);
+    if (mine) tile_epilogue<BM, BN, GNM, Cfg<BM, BN, BK, S>::LDS>(p, smem, m0, n0, acc, pre);
     it += ke - kb;
     __syncthreads();  // the ring / epilogue tile is free before the next segment's LDS-DMA
   }
@@ -1051,6 +1166,33 @@ struct HaloBlock {
   // compute cursor: the current chunk's halo slot and the current weight slot
   int cpar, wslot;
   f32x4 acc[MI][NJ];
+  // epilogue operands loaded ahead (EpiPre): at kernel start where the row operands fit the registers
+  static constexpr int GPR = WN / 8;
+  static constexpr int RMAX = (WM * GPR + 63) / 64;
+  static constexpr bool kEarly = RMAX <= 4;
+  EpiPre<NJ, RMAX> pre;
+  __device__ __forceinline__ long out_pix(int row) const {   // output pixel of wave row `row` (-1: outside)
+    const int pl = wm * WM + row;
+    const int ty = pl / TW, tx = pl - (pl / TW) * TW;
+    const int oy = oy0 + ty, ox = ox0 + tx;
+    if (pl >= C::BM || oy >= p.hout || ox >= p.wout) return -1;
+    return ((long)frame * p.hout + oy) * p.wout + ox;
+  }
+  __device__ __forceinline__ void epi_load_rows() {
+    if (GNM != 0) return;
+    const int c = n0 + wn * WN + (lane % GPR) * 8;
+    const bool full = c + 8 <= p.cout;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const int g = lane + 64 * r;
+      pre.mrow[r] = (g < WM * GPR && c < p.cout) ? out_pix(g / GPR) : -1;
+      if (pre.mrow[r] >= 0 && full) {
+        if (p.resid) pre.res[r] = *reinterpret_cast<const bf16x8*>(p.resid + pre.mrow[r] * p.ldr + c);
+        if (p.mask) pre.msk[r] = *reinterpret_cast<const bf16x8*>(p.mask + pre.mrow[r] * p.ldmask + c);
+      }
+    }
+    if (p.rowbias && full) pre.rb = *reinterpret_cast<const bf16x8*>(p.rowbias + (long)(*p.rowbias_idx) * p.rowbias_ld + c);
+  }
 
   __device__ __forceinline__ void issue_halo(int c) {
     DC_LDS char* hb = (DC_LDS char*)smem + ((c - c_begin) & 1) * C::HALO;
@@ -1206,6 +1348,11 @@ struct HaloBlock {
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the epilogue's column (and, where registers allow, row) operands in flight under the main loop
+    if (!(p.diag & 256)) {
+      epi_cols<0>(p, n0 + wn * WN + (lane & 15), pre);
+      if (kEarly) epi_load_rows();
+    }
 
     q_c = c_begin;
     q_t = 0;
@@ -1236,13 +1383,14 @@ struct HaloBlock {
   __device__ __forceinline__ void epilogue() {
     const int wid = threadIdx.x >> 6;
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;
+    if (!kEarly || (p.diag & 256)) epi_load_rows();
+    if (p.diag & 256) epi_cols<0>(p, n0 + wn * WN + (lane & 15), pre);   // A/B: the late (round-3) placement
     __syncthreads();
     constexpr int LDE = WN + 8;
     bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int c = n0 + wn * WN + j * 16 + col_l;
-      const float bv = (p.bias && c < p.cout) ? p.bias[c] : 0.0f;
+      const float bv = pre.cv[j];
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1266,17 +1414,14 @@ struct HaloBlock {
       return;
     }
     if (p.diag & 64) return;   // experiments only: no epilogue stores
-#pragma unroll 4
-    for (int g = lane; g < WM * GPR; g += 64) {
-      const int row = g / GPR, cg = g - (g / GPR) * GPR;
-      const int pl = wm * WM + row;
-      const int c = n0 + wn * WN + cg * 8;
-      const int ty = pl / TW, tx = pl - (pl / TW) * TW;
-      const int oy = oy0 + ty, ox = ox0 + tx;
-      if (pl >= C::BM || oy >= p.hout || ox >= p.wout || c >= p.cout) continue;
+    const int cg = lane % GPR, c = n0 + wn * WN + cg * 8;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      if (pre.mrow[r] < 0) continue;
+      const int row = (lane + 64 * r) / GPR;
       float v[8];
       load8(es + row * LDE + cg * 8, v);
-      epilogue_store(p, ((long)frame * p.hout + oy) * p.wout + ox, c, v, false);
+      epilogue_store_pre(p, pre, r, c, v);
     }
   }
 };
