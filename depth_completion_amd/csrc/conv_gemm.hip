@@ -12,7 +12,7 @@ int conv_launch_resident(int i, ConvGemmParams& p, int bpc, hipStream_t s);
 // external algo ids: 1 .. kNumAll im2col / halo variants (conv_gemm_impl.h), then the weight-streaming skinny variants,
 // then the weight-resident persistent narrow convs (conv_skinny.h), then the wide im2col tiles (conv_gemm_impl.h)
 static_assert(kNumAll + kNumSkinny + kNumResident + 1 == kWideFirst, "external algo id blocks");
-constexpr int kNumExt = kWideFirst + kNumWide - 1;
+constexpr int kNumExt = kHaloXFirst + kNumHaloX - 1;
 extern "C" int dc_conv_num_algos(void) { return kNumExt; }
 
 extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
@@ -146,7 +146,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
     }
     return conv_launch_algo_ln(algo_index(algo), p, M, splits, smallc, s);
   }
-  if (algo >= kWideFirst) {
+  if (algo >= kWideFirst && !algo_is_halo(algo)) {
     // wide im2col tile: the launch below (algo_index maps it into kAlgos).  No fused-GroupNorm form: a GroupNorm-fused
     // call that carries a wide choice (the table's entry is shared with the shape's unfused calls, and a shape is
     // tuned before its GroupNorm consumers register) runs the 64 x 64 double-buffered tile, the level-0 winner before
@@ -154,7 +154,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
       algo = 13;
       splits = 1;
     }
-  } else if (algo > kNumAll + kNumSkinny) {
+  } else if (algo > kNumAll + kNumSkinny && algo < kWideFirst) {
     const int ri = algo - kNumAll - kNumSkinny - 1;
     if (resident_eligible(p)) return conv_launch_resident(ri, p, splits, s);
     algo = 0;   // outside the narrow-conv contract (nearest-shape pick): im2col heuristic
@@ -170,7 +170,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   }
   if (algo_is_halo(algo)) {
     if (halo_eligible(p)) {
-      const int hi = algo - kNumBase - 1;
+      const int hi = halo_index(algo);
       const int hs = splits == 0 ? 1 : splits;
       return p.gn.mode == 1 ? conv_launch_halo_gn(hi, p, hs, s)
            : p.gn.mode == 2 ? conv_launch_halo_gnb(hi, p, hs, s) : launch_halo_idx<0>(hi, p, hs, s);

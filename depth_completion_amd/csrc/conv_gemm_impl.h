@@ -1453,6 +1453,15 @@ constexpr HaloAlgo kHaloAlgos[] = {
     {4, 32, 64, 2, 2, 3, 1},
     {8, 32, 64, 4, 1, 8, 1},
     {6, 24, 64, 1, 4, 6, 1},
+    // (round 4, external ids 62 ..) 192-px tiles at one block per CU with an 8-deep weight ring: at batch 1 the level-0
+    // frame (72 x 96) is 36 such tiles, x 5 column tiles = 180 blocks, all resident at once (the 128-px tiles give 270
+    // blocks, more than the CUs at one block each, so they run two blocks per CU on a 3-deep ring and the weight stream
+    // keeps ~16 KB per CU in flight); 4 x 1 waves of 48 / 64 px x 64 channels
+    {4, 48, 64, 4, 1, 8, 1},    // 6 x 50 halo (144 KB)
+    {6, 32, 64, 4, 1, 8, 1},    // 8 x 34 halo (136 KB)
+    {8, 24, 64, 4, 1, 8, 1},    // 10 x 26 halo (136 KB)
+    {4, 48, 64, 4, 1, 8, 0},
+    {6, 32, 64, 4, 1, 8, 0},
 };
 
 constexpr long kCounterBytes = 64 * 1024;
@@ -1482,19 +1491,25 @@ constexpr Algo kAlgos[] = {{0, 0, 0, 0},       {128, 128, 64, 4}, {128, 64, 64, 
 // kAlgos, kNumBase + 1 .. kNumBase + kNumHalo the halo variants, then the later kAlgos entries.
 constexpr int kNumAlgos = 28;   // kAlgos entries behind external ids 1 .. kNumAll (the wide tiles come after)
 constexpr int kNumBase = 22;
-constexpr int kNumHalo = sizeof(kHaloAlgos) / sizeof(kHaloAlgos[0]);
+constexpr int kNumHalo = 14;   // halo variants behind external ids kNumBase + 1 .. kNumBase + kNumHalo
+constexpr int kNumHaloX = sizeof(kHaloAlgos) / sizeof(kHaloAlgos[0]) - kNumHalo;   // ... and behind kHaloXFirst ..
 constexpr int kNumAll = kNumAlgos + kNumHalo;
 // the wide tiles (kAlgos[kNumAlgos + 1 ..]) take the external ids after the skinny (43 .. 54) and resident (55 .. 58)
 // variants of conv_skinny.h (conv_gemm.hip checks the numbering)
 constexpr int kWideFirst = 59;
 constexpr int kNumWide = sizeof(kAlgos) / sizeof(kAlgos[0]) - 1 - kNumAlgos;
 static_assert(kNumAll == 42, "external algo ids of the tuned tables");
-__host__ __device__ constexpr bool algo_is_halo(int id) { return id > kNumBase && id <= kNumBase + kNumHalo; }
+constexpr int kHaloXFirst = kWideFirst + kNumWide;   // 62: the round-4 halo variants
+__host__ __device__ constexpr bool algo_is_halo(int id) {
+  return (id > kNumBase && id <= kNumBase + kNumHalo) || (id >= kHaloXFirst && id < kHaloXFirst + kNumHaloX);
+}
+// kHaloAlgos index of a halo external id
+__host__ __device__ constexpr int halo_index(int id) { return id < kHaloXFirst ? id - kNumBase - 1 : kNumHalo + id - kHaloXFirst; }
 // kAlgos index of an im2col external id
 __host__ __device__ constexpr int algo_index(int id) {
   return id <= kNumBase ? id : (id <= kNumAll ? id - kNumHalo : id - kWideFirst + kNumAlgos + 1);
 }
-static_assert(kNumHalo == 14, "DC_HALO cases below");
+static_assert(kNumHalo + kNumHaloX == 19, "DC_HALO cases below");
 
 template <int TH, int TW, int BN, int WGM, int WGN, int S, int SCHED, int GNM>
 int launch_halo(ConvGemmParams& p, int splits, hipStream_t stream) {
@@ -1596,7 +1611,8 @@ int launch_halo_idx(int i, ConvGemmParams& p, int splits, hipStream_t s) {
     return launch_halo<kHaloAlgos[i].th, kHaloAlgos[i].tw, kHaloAlgos[i].bn, kHaloAlgos[i].wgm, kHaloAlgos[i].wgn, \
                        kHaloAlgos[i].s, kHaloAlgos[i].sched, GNM>(p, splits, s);
     DC_HALO(0) DC_HALO(1) DC_HALO(2) DC_HALO(3) DC_HALO(4) DC_HALO(5) DC_HALO(6) DC_HALO(7) DC_HALO(8)
-    DC_HALO(9) DC_HALO(10) DC_HALO(11) DC_HALO(12) DC_HALO(13)
+    DC_HALO(9) DC_HALO(10) DC_HALO(11) DC_HALO(12) DC_HALO(13) DC_HALO(14) DC_HALO(15) DC_HALO(16) DC_HALO(17)
+    DC_HALO(18)
 #undef DC_HALO
     default: return DC_ERR_ARG;
   }

@@ -193,7 +193,8 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
 HALO_FIRST, HALO_LAST = 23, 36   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv (conv_gemm_impl.h); ids
 # 1 .. 22 and 37 .. 42 are im2col tile variants, SKINNY_FIRST .. dc_conv_num_algos() the weight-streaming skinny
 # conv / linear variants (conv_skinny.h)
-IM2COL_LAST, SKINNY_FIRST, RESIDENT_FIRST, WIDE_FIRST = 42, 43, 55, 59   # RESIDENT_FIRST ..: the weight-resident
+HALOX_FIRST, HALOX_LAST = 62, 66   # the round-4 halo variants (192-px tiles, one block per CU, 8-deep weight ring)
+IM2COL_LAST, SKINNY_FIRST, RESIDENT_FIRST, WIDE_FIRST, WIDE_LAST = 42, 43, 55, 59, 61   # RESIDENT_FIRST ..: the weight-resident
 # persistent narrow convs (cin 64, cout <= 64; their split field is the persistent grid's blocks per CU); WIDE_FIRST ..
 # dc_conv_num_algos(): im2col tiles holding 320 output channels per block
 SKINNY_TAPS = (9, 9, 9, 9, 9, 1, 1, 1, 1, 1, 1, 1)   # taps of skinny variant SKINNY_FIRST + i (conv_skinny.h kSkinnyAlgos)
@@ -239,11 +240,11 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     nalg = _lib.load().dc_conv_num_algos()
     # im2col tiles: split-K 1..32, and stream-K over 256 / 512 / 768 blocks (splitk -1 / -2 / -3); halo tiles
     # (algos > HALO_FIRST - 1, stride-1 3x3 convs over whole 64-channel chunks only): input-chunk splits
-    gemm_ids = list(range(1, HALO_FIRST)) + list(range(HALO_LAST + 1, IM2COL_LAST + 1)) + list(range(WIDE_FIRST, nalg + 1))
+    gemm_ids = list(range(1, HALO_FIRST)) + list(range(HALO_LAST + 1, IM2COL_LAST + 1)) + list(range(WIDE_FIRST, WIDE_LAST + 1))
     cands = [(0, 0)] + [(a, s) for a in gemm_ids for s in (1, 2, 4, 8, 12, 16, 24, 32, -1, -2, -3)]
     if halo_eligible(d):
-        cands += [(a, s) for a in range(HALO_FIRST, HALO_LAST + 1) for s in (1, 2, 3, 4, 5, 8, 10, 16, 20)
-                  if s <= d.cin // 64]
+        cands += [(a, s) for a in list(range(HALO_FIRST, HALO_LAST + 1)) + list(range(HALOX_FIRST, HALOX_LAST + 1))
+                  for s in (1, 2, 3, 4, 5, 8, 10, 16, 20) if s <= d.cin // 64]
     if skinny_eligible(d):
         # skinny variants (an ineligible variant reports an error or falls back; both are timed like the rest)
         taps = d.kh * d.kw

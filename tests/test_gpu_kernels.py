@@ -610,7 +610,8 @@ def test_conv_all_algos(ctx, algo, nsplit):
         assert rel(nchw(y, n, ho, wo), ref) < 1e-2, (algo, nsplit, n, cin, cout, h, w, stride, mode)
 
 
-HALO_ALGOS = list(range(23, 37))   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv (conv_gemm.hip)
+HALO_ALGOS = list(range(23, 37)) + list(range(62, 67))   # dc_conv_gemm algo ids of the halo-tile direct 3x3 conv
+# (conv_gemm.hip; 62 ..: the round-4 192-px deep-ring variants)
 
 
 @pytest.mark.parametrize("algo", HALO_ALGOS)
@@ -661,7 +662,7 @@ def test_conv_halo_algos(ctx, algo, nsplit):
 SKINNY_FIRST, SKINNY_LAST = 43, 54   # dc_conv_gemm algo ids of the weight-streaming skinny variants (conv_skinny.h)
 SKINNY_ALGOS = list(range(SKINNY_FIRST, SKINNY_LAST + 1))
 RESIDENT_FIRST, RESIDENT_LAST = 55, 58   # ... of the weight-resident persistent narrow convs (conv_skinny.h)
-NUM_ALGOS = 61   # dc_conv_num_algos(): ... and the wide im2col tiles 59 .. 61 (conv_gemm_impl.h)
+NUM_ALGOS = 66   # 1 .. 61 (round 3) and the round-4 halo variants 62 .. 66
 
 
 @pytest.mark.parametrize("algo", list(range(RESIDENT_FIRST, RESIDENT_LAST + 1)))

@@ -30,7 +30,8 @@ TAESD = [(1, 72, 96, 64, 72, 96, 64, 0), (1, 72, 96, 64, 144, 192, 64, 1), (1, 1
          (8, 72, 96, 320, 72, 96, 320, 0), (8, 36, 48, 640, 36, 48, 640, 0)]
 
 
-def run(ctx, d, reps):
+def run(ctx, d, reps, wts=None):
+    """reps launches in one graph; wts: weight copies cycled over the launches (weights cold, as in the step)"""
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -39,9 +40,13 @@ def run(ctx, d, reps):
             _lib.call("dc_conv_gemm", ctx_desc(d), torch.cuda.current_stream().cuda_stream)
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
+    w0 = d.w
     with torch.cuda.graph(g):
-        for _ in range(reps):
+        for i in range(reps):
+            if wts:
+                d.w = wts[i % len(wts)].data_ptr()
             _lib.call("dc_conv_gemm", ctx_desc(d), torch.cuda.current_stream().cuda_stream)
+    d.w = w0
     g.replay()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -60,11 +65,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--set", default="all")
+    ap.add_argument("--algos", type=int, nargs="*", default=None)
+    ap.add_argument("--cold", type=int, default=0, help="weight copies cycled over the launches (0: one, warm)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     ctx = Ctx(dev)
     nalg = _lib.load().dc_conv_num_algos()
-    halo = list(range(23, nalg + 1))
+    halo = args.algos or list(range(23, nalg + 1))
     shapes = {"c2": C2, "taesd": TAESD, "all": C2 + TAESD}[args.set]
     for nb, hin, win, cin, hout, wout, cout, mode in shapes:
         x = torch.randn(nb * hin * win, cin, device=dev).to(torch.bfloat16)
@@ -74,8 +81,9 @@ def main():
         y0 = torch.zeros(nb * hout * wout, ldy, device=dev, dtype=torch.bfloat16)
         d = ops.conv_desc(ctx, x, wt, nb=nb, hin=hin, win=win, cin=cin, hout=hout, wout=wout, cout=cout, mode=mode,
                           bias=b, y=y0)
+        wts = [wt] + [wt.clone() for _ in range(args.cold - 1)] if args.cold > 1 else None
         tuned = (d.algo, d.splitk)
-        t0 = run(ctx, d, args.reps)
+        t0 = run(ctx, d, args.reps, wts)
         ref = y0.clone()
         flops = 2.0 * nb * hout * wout * cout * 9 * cin
         best = (float("inf"), None, 0.0)
@@ -86,7 +94,7 @@ def main():
                     continue
                 d.algo, d.splitk = a, sp
                 y0.zero_()
-                t = run(ctx, d, args.reps)
+                t = run(ctx, d, args.reps, wts)
                 err = float((y0.float() - ref.float()).norm() / ref.float().norm())
                 if err > 2e-2:
                     print(f"   !! algo {a} split {sp}: rel err {err:.3e}", flush=True)
