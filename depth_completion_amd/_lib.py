@@ -73,6 +73,7 @@ _SIGS = {
                          vp, i32, vp, vp],
     "dc_gn_acc_bytes": [i32, i32],
     "dc_gn_fuse_pays": [i32, i32, i32, i32],
+    "dc_gn_coop_timeouts": [],
     "dc_groupnorm_fwd_acc": [vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp, vp],
     "dc_groupnorm_bwd_acc": [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp, i32,
                              vp, i32, vp],

@@ -161,6 +161,10 @@ int dc_groupnorm_bwd_acc(const void* x, int ldx, const void* x2, int ldx2, int c
                          const float* gamma, const float* stats, const long long* acc, const void* dyp, int lddy,
                          void* dx, int lddx, const void* add1, int ldadd1, const void* add2, int ldadd2,
                          void* stream);
+/* count of spin bounds reached by the cooperative single-launch GroupNorm since load (8 blocks per (frame, group)
+ * meeting at an arrival counter; opt-in with DC_GN_COOP=1 for UNet level-2 / 3 slices at up to 4 frames; by default one
+ * block per group): 0 unless the blocks of a group were not resident together (tests check it) */
+int dc_gn_coop_timeouts(void);
 int dc_layernorm_fwd(const void* x, int ldx, long long rows, int c, float eps, const float* gamma, const float* beta,
                      void* y, int ldy, float* stats, void* stream);
 /* gamma NULL: dy is already gamma * dL/dy (the input-gradient of a dc_ln_fuse folded weight) */

@@ -194,13 +194,15 @@ def test_small_cin_and_splitk_linear(ctx):
 
 
 # ----------------------------------------------------------------------------- norms
-@pytest.fixture(params=["group", "2pass", "3pass"])
+@pytest.fixture(params=["group", "group1", "2pass", "3pass"])
 def gn_path(request, monkeypatch):
-    """GroupNorm launch form: one block per (frame, group) in a single launch wherever the slice fits
-    the LDS (DC_GN_GROUP=-1; by default only small slices take it), stats + apply with the finalize folded
-    into every apply block (DC_GN_GROUP=0), or stats / finalize / apply (DC_GN_GROUP=0, DC_GN_FUSED=0)."""
-    monkeypatch.setenv("DC_GN_GROUP", "-1" if request.param == "group" else "0")   # -1: no size cap
+    """GroupNorm launch form: a single launch wherever the slice fits the LDS (DC_GN_GROUP=-1; by default only
+    small slices take it) -- 8 cooperating blocks per (frame, group) where their rows fit the registers ("group"),
+    or one block per (frame, group) ("group1", DC_GN_COOP=0) --, stats + apply with the finalize folded into every
+    apply block (DC_GN_GROUP=0), or stats / finalize / apply (DC_GN_GROUP=0, DC_GN_FUSED=0)."""
+    monkeypatch.setenv("DC_GN_GROUP", "-1" if request.param.startswith("group") else "0")   # -1: no size cap
     monkeypatch.setenv("DC_GN_FUSED", "0" if request.param == "3pass" else "1")
+    monkeypatch.setenv("DC_GN_COOP", "0" if request.param == "group1" else "1")   # (cooperative form: opt-in)
     return request.param
 
 
@@ -297,6 +299,46 @@ def test_groupnorm_paths_agree(ctx, monkeypatch, n, h, w, c, two):
     assert rel(s3, s2) < 1e-6
     assert rel(y3, y2) < 2e-3
     assert rel(d3, d2) < 5e-3
+
+
+@pytest.mark.parametrize("n,h,w,c,two", [(1, 18, 24, 1280, False), (1, 18, 24, 1920, True), (1, 18, 24, 640, False),
+                                        (1, 9, 12, 2560, True), (1, 9, 12, 1280, False), (2, 18, 24, 960, True),
+                                        (4, 9, 12, 1280, False)])
+def test_groupnorm_coop(ctx, monkeypatch, n, h, w, c, two):
+    """The cooperative single-launch GroupNorm (8 blocks per (frame, group) exchanging fp64 partials through an
+    arrival counter) at the UNet level-2 / 3 shapes: against torch fp32, against the one-block-per-group kernel
+    (the same fp32 inputs folded in another order), bit-identical on repeat, and no spin bound ever reached."""
+    from depth_completion_amd import _lib, ops
+    x = (rnd(n, c, h, w, seed=47) * 1.5 + 0.4).to(torch.bfloat16).float().requires_grad_(True)
+    gamma = (1 + 0.1 * rnd(c, seed=48)).to(torch.bfloat16).float()
+    beta = (0.1 * rnd(c, seed=49)).to(torch.bfloat16).float()
+    ref = F.silu(F.group_norm(x, 32, gamma, beta, eps=1e-5))
+    gyf = rnd(n, c, h, w, seed=50)
+    ref.backward(gyf)
+    xs = nhwc(x.detach())
+    c1 = (c // 2) // 64 * 64 if two else 0
+    xa, xb = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if two else (xs, None)
+    kw = dict(x2=xb, c1=c1) if two else {}
+    gy, add = nhwc(gyf), nhwc(rnd(n, c, h, w, seed=51))
+    monkeypatch.setenv("DC_GN_GROUP", "-1")
+    t0 = _lib.load().dc_gn_coop_timeouts()
+    res = {}
+    for path in ("coop", "coop2", "one"):
+        monkeypatch.setenv("DC_GN_COOP", "0" if path == "one" else "1")
+        y = torch.empty_like(xs)
+        stats = torch.empty(n, 32, 2, device=dev)
+        dx = torch.empty_like(xs)
+        ops.groupnorm(ctx, xa, n, h * w, c, gamma, beta, 1e-5, True, y, stats, **kw)
+        ops.groupnorm_bwd(ctx, xa, n, h * w, c, gamma, beta, True, stats, gy, dx, add1=add, **kw)
+        torch.cuda.synchronize()
+        res[path] = (y, stats, dx)
+    assert _lib.load().dc_gn_coop_timeouts() == t0
+    (y1, s1, d1), (y2, s2, d2), (y3, s3, d3) = res["coop"], res["coop2"], res["one"]
+    assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(d1, d2)
+    assert rel(s1, s3) < 1e-5
+    assert rel(y1, y3) < 2e-3 and rel(d1, d3) < 5e-3
+    assert rel(nchw(y1, n, h, w), ref) < 1e-2
+    assert rel(nchw(d1, n, h, w), x.grad + nchw(add, n, h, w)) < 2e-2
 
 
 @pytest.mark.parametrize("c", [64, 320, 1280])
