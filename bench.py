@@ -192,7 +192,8 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
     from oracle import pipeline_ref as P
     from oracle.diffusers_ref import (AutoencoderTiny, DDIMScheduler, UNet2DConditionModel, synthetic_state_dict,
                                       synthetic_taesd_state_dict, synthetic_text_embedding)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    # every CPU this process may run on (the reference's CPU path on the host's cores)
+    threads = len(os.sched_getaffinity(0))
     torch.set_num_threads(threads)
     unet = UNet2DConditionModel()
     unet.load_state_dict(synthetic_state_dict(unet, 11))
@@ -211,7 +212,8 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
     t_fixed = max(times[1] - t_step, 0.0)
     t_frame = (t_fixed + steps * t_step) * seeds
     return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads,
-            "cores_label": f"{threads} threads used of {os.cpu_count()} host CPUs visible", "kind": "port",
+            "cores_label": f"{threads} threads = CPUs in this process's affinity mask ({os.cpu_count()} host CPUs)",
+            "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"oracle bf16 CPU pipeline, 1 frame {w}x{h}, 1- and 2-step calls "
                       f"({times[1]:.1f}s, {times[2]:.1f}s) extrapolated to {steps} guided steps x {seeds} seed(s) "

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of environment settings on the C2 bench (GPU box), each line "name|ENV=.. ENV2=..":
-#   bash tools/ab_env.sh "base|" "korder|DC_KORDER=1" ...
+#   bash tools/ab/ab_env.sh "base|" "korder|DC_KORDER=1" ...
 set -e
 mkdir -p gpurun_out/ab
 for spec in "$@"; do

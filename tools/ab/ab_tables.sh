@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of GEMM tables on the C2 bench (GPU box): bash tools/ab_tables.sh tools/ab/a.json tools/ab/b.json ...
+# A/B of GEMM tables on the C2 bench (GPU box): bash tools/ab/ab_tables.sh tools/ab/a.json tools/ab/b.json ...
 set -e
 mkdir -p gpurun_out/ab
 for t in "$@"; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of environment settings on the C2 bench line, alternating on one box (2 rounds):
-#   bash tools/env_ab.sh <tag> "" "DC_GN_GROUP=0" ...      ("" = the defaults)
+#   bash tools/ab/env_ab.sh <tag> "" "DC_GN_GROUP=0" ...      ("" = the defaults)
 set -e
 tag=${1:?tag}; shift
 out=gpurun_out/$tag

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes of the dominant kernel (conv_gemm) over an eager bench step (4 denoising steps):
-# FETCH_SIZE, WRITE_SIZE and the MFMA-busy pass, for one batch size.  Usage: bash tools/gpu_prof2.sh <tag> <batch>
+# FETCH_SIZE, WRITE_SIZE and the MFMA-busy pass, for one batch size.  Usage: bash tools/ab/gpu_prof2.sh <tag> <batch>
 set -e
 tag=${1:-run}; batch=${2:-1}
 out=gpurun_out/$tag/b$batch

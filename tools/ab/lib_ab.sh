@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two prebuilt libdcamd.so builds (DC_LIB) on a python script and the C2 bench (GPU box):
-#   bash tools/lib_ab.sh <tag> "<script args>" ab/lib_a.so ab/lib_b.so ...
+#   bash tools/ab/lib_ab.sh <tag> "<script args>" ab/lib_a.so ab/lib_b.so ...
 set -e
 tag=${1:?tag}; script=$2; shift 2
 out=gpurun_out/$tag

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Re-tune the stride-1 3x3 shapes (halo kernel candidates included) with cold caches, then A/B the C2 / C3 bench
-# lines old table vs new table on the same box, alternating.  Usage: bash tools/retune_ab.sh <tag>
+# lines old table vs new table on the same box, alternating.  Usage: bash tools/ab/retune_ab.sh <tag>
 set -e
 tag=${1:?tag}
 out=gpurun_out/$tag

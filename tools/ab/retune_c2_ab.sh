@@ -1,7 +1,7 @@
 #!/bin/bash
 # Re-tune every C2 shape with DC_TUNE_COLD=<mode> (2: caches flushed, then the activation operands read back --
 # the step's cache state, weights cold / inputs warm), then A/B the C2 bench line old vs new table, alternating.
-# Usage: bash tools/retune_c2_ab.sh <tag> <cold mode>
+# Usage: bash tools/ab/retune_c2_ab.sh <tag> <cold mode>
 set -e
 tag=${1:?tag}
 mode=${2:-2}

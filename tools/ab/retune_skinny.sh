@@ -1,7 +1,7 @@
 #!/bin/bash
 # Cold-weight re-tune (DC_TUNE_COLD=2: caches flushed, then the activations read back, the step's state) of the few-pixel shapes (C2 / C4 at batch 1) with the weight-streaming skinny variants as candidates
 # (tools/tune_gemm.py --try: the committed choice against the skinny ids only), then A/B the C2 / C4 bench lines old
-# table vs new table on the same box, alternating.  Usage: bash tools/retune_skinny.sh <tag>
+# table vs new table on the same box, alternating.  Usage: bash tools/ab/retune_skinny.sh <tag>
 set -e
 tag=${1:?tag}
 out=gpurun_out/$tag

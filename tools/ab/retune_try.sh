@@ -2,7 +2,7 @@
 # Re-time every conv shape of the workloads: its committed choice against the given algo ids only (tune_gemm.py
 # --try), in the step's cache state (DC_TUNE_COLD=2: weights cold, activations warm), then A/B bench lines old table
 # vs new table on the same box, alternating.
-#   bash tools/retune_try.sh <tag> "<algo ids>" [workloads] [bench args]
+#   bash tools/ab/retune_try.sh <tag> "<algo ids>" [workloads] [bench args]
 set -e
 tag=${1:?tag}
 ids=${2:?algo ids}

@@ -2,7 +2,7 @@
 # Full re-tune of every conv shape of the given workloads (all algo ids, all splits: tune_gemm.py --try with every
 # id) in the step's cache state -- weights cold, activations warm (DC_TUNE_COLD=2) -- then A/B a bench line old table
 # vs new table on the same box, alternating.
-#   bash tools/retune_warm_act.sh <tag> [workloads] [bench args]     e.g.  r03w8 "c2:8" "--batch 8 --steps 2 --warmup 1"
+#   bash tools/ab/retune_warm_act.sh <tag> [workloads] [bench args]     e.g.  r03w8 "c2:8" "--batch 8 --steps 2 --warmup 1"
 set -e
 tag=${1:?tag}
 wl=${2:-c2:1}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Re-time every shape of the given workloads: the committed choice against the listed algo ids only (cold caches),
 # then A/B the C2 (and C3 batch-8) bench lines with the committed vs the new table, alternating.
-# Usage: bash tools/try_variants_ab.sh <tag> "<workloads>" <algo ids...>
+# Usage: bash tools/ab/try_variants_ab.sh <tag> "<workloads>" <algo ids...>
 set -e
 tag=${1:?tag}
 wls=${2:?workloads}
