@@ -592,6 +592,289 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   }
 }
 
+// ------------------------------------------------------------------------ forward, ping-pong
+// Two waves per SIMD in opposite phases (MI355X_MICROARCH.md "Two waves per SIMD"): 8-wave blocks, one per
+// CU, each wave holding 32 queries of a 256-query block; all 8 waves share one K / V LDS-DMA ring.  The
+// waves 0-3 (half A) and 4-7 (half B, on the same four SIMDs) run the same per-tile program one segment
+// apart, block barriers between segments, so in every segment one wave of each SIMD is in its MFMA phase
+// (S^T of tile t = K Q^T, and O^T += V^T P^T of tile t - 1: 16 MFMAs, LDS fragments read by asm with counted
+// lgkm waits) while its partner runs the softmax of its own tile on the VALU (max, lazy rescale, exp2, row
+// sum, bf16 pack) -- the phases that the one-barrier-per-tile kernel above runs in lockstep on every wave.
+// Work is dealt out stream-K over (256-query block, key tile) in equal ranges, one block per CU; a query
+// block cut between blocks is folded by the last arriver (sk_handoff_fwd).  Numerics as fwd_segment's
+// (fp32 row sums of the unrounded weights, FWD_TAU lazy rescale, query pre-scaled by 1/8).
+constexpr int PP_S = 4;                   // K + V ring stages: tile u + 2 is issued while tile u is consumed
+constexpr int PP_STAGE = 2 * TILE_B;      // 16 KB: K tile then V tile
+constexpr int PP_QPB = 256;               // queries per block unit (8 waves x 32)
+
+template <int IMM>
+__device__ __forceinline__ bf16x8 ds_read128_nw(unsigned addr) {
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(IMM));
+  return r;
+}
+
+struct PpState {
+  bf16x8 qf[4];
+  f32x16 oacc[2], sacc[2];
+  bf16x8 pf[4];
+  float m, l;
+};
+
+// MFMA phase of tile t: QK of tile t (stage KST) and PV of tile t - 1 (stage VST); QK / PV present or not.
+// LDS reads by asm in consumption order, at most 12 in flight (lgkmcnt counts to 15), each group waited
+// for just before its MFMAs: K rows of key half 0 / 1, then the V^T k-slices 0..3 (2 fragments each).
+template <bool QK, bool PV, int KST, int VST>
+__device__ __forceinline__ void pp_mfma(PpState& w, const unsigned (&ka)[2][4], const unsigned (&va)[4][2][2]) {
+  constexpr int KI = KST * PP_STAGE;
+  constexpr int VI = VST * PP_STAGE + TILE_B;
+  bf16x8 kf[2][4], vf[4][2];
+  auto vread = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db) vf[s][db] = trans_frag_nw<VI>(va[s][db][0], va[s][db][1]);
+  };
+  auto qk = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w.sacc[b][r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) w.sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[b][s], w.qf[s], w.sacc[b], 0, 0, 0);
+  };
+  auto pv = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+      w.oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], w.pf[s], w.oacc[db], 0, 0, 0);
+  };
+  if constexpr (QK) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kf[b][s] = ds_read128_nw<KI>(ka[b][s]);
+  }
+  if constexpr (QK && PV) {
+    vread(0);                                                     // K0 K1 V0 in flight
+    lgkm_wait<8>(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
+    qk(0);
+    vread(1);                                                     // K1 V0 V1
+    lgkm_wait<8>(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
+    qk(1);
+    vread(2);                                                     // V0 V1 V2
+  } else if constexpr (QK) {
+    lgkm_wait<4>(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
+    qk(0);
+    lgkm_wait<0>(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
+    qk(1);
+  } else {
+    vread(0);
+    vread(1);
+    vread(2);
+  }
+  if constexpr (PV) {
+    lgkm_wait<8>(vf[0][0], vf[0][1]);
+    pv(0);
+    vread(3);                                                     // V1 V2 V3
+    lgkm_wait<8>(vf[1][0], vf[1][1]);
+    pv(1);
+    lgkm_wait<4>(vf[2][0], vf[2][1]);
+    pv(2);
+    lgkm_wait<0>(vf[3][0], vf[3][1]);
+    pv(3);
+  }
+}
+
+// VALU phase of key tile kt: masked tail, row max, lazy rescale of (O, l), exp2, fp32 row sum, P -> bf16
+__device__ __forceinline__ void pp_softmax(PpState& w, int kt, int T, int hh) {
+  if ((kt + 1) * 64 > T) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (key >= T) w.sacc[b][r] = -INFINITY;
+      }
+  }
+  float mx0 = fmaxf(w.sacc[0][0], fmaxf(w.sacc[0][1], w.sacc[0][2]));
+  float mx1 = fmaxf(w.sacc[1][0], fmaxf(w.sacc[1][1], w.sacc[1][2]));
+#pragma unroll
+  for (int r = 3; r < 15; r += 2) {
+    mx0 = fmaxf(mx0, fmaxf(w.sacc[0][r], w.sacc[0][r + 1]));
+    mx1 = fmaxf(mx1, fmaxf(w.sacc[1][r], w.sacc[1][r + 1]));
+  }
+  float mx = fmaxf(fmaxf(mx0, w.sacc[0][15]), fmaxf(mx1, w.sacc[1][15]));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  if (__any(mx > w.m + FWD_TAU)) {
+    const float mnew = fmaxf(w.m, mx);
+    const float alpha = fast_exp2((w.m - mnew) * LOG2E);
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) w.oacc[db][r] *= alpha;
+    w.l *= alpha;
+    w.m = mnew;
+  }
+  const float ml = w.m * LOG2E;
+  float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pv = fast_exp2(fmaf(w.sacc[b][r], LOG2E, -ml));
+      w.sacc[b][r] = pv;
+      ps[(b << 1) | (r & 1)] += pv;
+    }
+  w.l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) w.pf[s] = acc_to_frag(w.sacc[s >> 1], s & 1);
+}
+
+__device__ __forceinline__ void fwd_pp_segment(char* smem, const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo,
+                                               float* lse, int qbk, int h, int n, int t0, int nt, const AttnSK& sk,
+                                               long bi, int seg, bool whole) {
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = threadIdx.x >> 6;
+  const int half = __builtin_amdgcn_readfirstlane(wid >> 2);   // 0: A, 1: B (one segment behind)
+  const int C = heads * 64;
+  const bf16* base = qkv + (long)n * T * ld;
+  const int my_q = qbk * PP_QPB + wid * 32 + (lane & 31);
+  const bool qok = my_q < T;
+  PpState w;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) w.qf[s] = load_row8(base + (long)my_q * ld + h * 64 + 16 * s + 8 * hh, qok, 0.125f);
+  w.m = -INFINITY;
+  w.l = 0.0f;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w.oacc[db][r] = 0.0f;
+
+  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
+  const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
+  TileDma<512> dma;
+  dma.init(threadIdx.x, ld);
+  auto issue = [&](int u) __attribute__((always_inline)) {
+    char* st = smem + (u % PP_S) * PP_STAGE;
+    dma.issue(rk, st, (t0 + u) * 64, T, ld, threadIdx.x);
+    dma.issue(rv, st + TILE_B, (t0 + u) * 64, T, ld, threadIdx.x);
+  };
+  const unsigned sb = lds_addr(smem);
+  unsigned ka[2][4], va[4][2][2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) ka[b][s] = sb + row_off(32 * b + (lane & 31), 2 * s + hh);
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const TrOff t = tr_off(16 * s, 32 * db, lane);
+      va[s][db][0] = sb + t.lo;
+      va[s][db][1] = sb + t.hi;
+    }
+  // prologue: tiles 0 and 1 in flight, tile 0 landed before segment 0
+  issue(0);
+  if (nt > 1) {
+    issue(1);
+    vm_wait_n<2>();
+  } else {
+    vm_wait_n<0>();
+  }
+  __syncthreads();
+
+  // segment s: half A is in its MFMA phase of tile s / 2 when s is even and in its softmax of tile (s - 1) / 2
+  // when s is odd; half B the same one segment later.  Ring: tile u + 2 is issued in segment 2u (its stage
+  // was last read by B's PV of tile u - 2 in segment 2u - 1) and waited for at the end of segment 2u + 3.
+  const int nseg = 2 * nt + 2;
+  auto segment = [&](int s, auto CC) __attribute__((always_inline)) {
+    constexpr int c = decltype(CC)::value;   // s % 8: the ring stages are compile-time per copy
+    if (s >= nseg) return;
+    if constexpr ((c & 1) == 0) {
+      if (s / 2 + 2 < nt) issue(s / 2 + 2);
+    }
+    if (half == 0) {
+      if constexpr ((c & 1) == 0) {
+        constexpr int KST = (c / 2) % PP_S, VST = (c / 2 + PP_S - 1) % PP_S;
+        const int t = s / 2;
+        if (t == 0) pp_mfma<true, false, KST, VST>(w, ka, va);
+        else if (t < nt) pp_mfma<true, true, KST, VST>(w, ka, va);
+        else pp_mfma<false, true, KST, VST>(w, ka, va);
+      } else {
+        const int t = (s - 1) / 2;
+        if (t < nt) pp_softmax(w, t0 + t, T, hh);
+      }
+    } else {
+      if constexpr ((c & 1) == 1) {
+        constexpr int KST = ((c - 1) / 2) % PP_S, VST = ((c - 1) / 2 + PP_S - 1) % PP_S;
+        const int t = (s - 1) / 2;
+        if (t == 0) pp_mfma<true, false, KST, VST>(w, ka, va);
+        else if (t < nt) pp_mfma<true, true, KST, VST>(w, ka, va);
+        else pp_mfma<false, true, KST, VST>(w, ka, va);
+      } else {
+        if (s >= 2) pp_softmax(w, t0 + (s - 2) / 2, T, hh);
+      }
+    }
+    if constexpr ((c & 1) == 1) {
+      // tile u = (s + 1) / 2 (A's next QK) landed; tile u + 1, issued in segment s - 1, may stay in flight
+      if ((s + 1) / 2 + 1 < nt) vm_wait_n<2>();
+      else vm_wait_n<0>();
+    }
+    __syncthreads();
+  };
+  for (int s0 = 0; s0 < nseg; s0 += 8) {
+    segment(s0, std::integral_constant<int, 0>{});
+    segment(s0 + 1, std::integral_constant<int, 1>{});
+    segment(s0 + 2, std::integral_constant<int, 2>{});
+    segment(s0 + 3, std::integral_constant<int, 3>{});
+    segment(s0 + 4, std::integral_constant<int, 4>{});
+    segment(s0 + 5, std::integral_constant<int, 5>{});
+    segment(s0 + 6, std::integral_constant<int, 6>{});
+    segment(s0 + 7, std::integral_constant<int, 7>{});
+  }
+  float m = w.m, l = w.l + __shfl_xor(w.l, 32, 64);
+  if (!whole) {   // query block shared with other blocks: merge (m, l, O) in block order
+    float v[34];
+    v[0] = m;
+    v[1] = l;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[2 + 16 * db + r] = w.oacc[db][r];
+    if (!sk_handoff_fwd<8>(sk, smem, bi, (T + 63) / 64, seg, v)) return;
+    m = v[0];
+    l = v[1];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) w.oacc[db][r] = v[2 + 16 * db + r];
+  }
+  const float inv = 1.0f / l;
+  if (qok) {
+    bf16* orow = o + ((long)n * T + my_q) * ldo + h * 64;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g2 = 0; g2 < 4; ++g2) {
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (bf16)(w.oacc[db][4 * g2 + e] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * g2 + 4 * hh) = v;
+      }
+    if (hh == 0) lse[((long)n * heads + h) * T + my_q] = m + logf(l);
+  }
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_pp_kernel(
+    const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse, AttnSK sk) {
+  __shared__ __attribute__((aligned(16))) char smem[PP_S * PP_STAGE];
+  const int ntk = (T + 63) / 64;
+  const int nqb = (T + PP_QPB - 1) / PP_QPB;
+  sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
+    const int qbk = (int)(bi % nqb);
+    const long nh = bi / nqb;
+    fwd_pp_segment(smem, qkv, ld, T, heads, o, ldo, lse, qbk, (int)(nh % heads), (int)(nh / heads), t0, cnt, sk, bi,
+                   seg, t0 == 0 && cnt == ntk);
+  });
+}
+
 // ------------------------------------------------------------------------------ backward
 // dK/dV: 32 QW keys per block resident in registers (32 per wave); KS query-splits per block (waves
 // QW p .. QW p + QW - 1 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a
@@ -1172,6 +1455,33 @@ bool launch_fwd_sk(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, i
                      lse, sk);
   return true;
 }
+
+// Ping-pong forward (attn_fwd_pp_kernel): one 8-wave block per CU, stream-K over (256-query block, key tile).
+// Default wherever every block gets >= 16 key tiles (UNet levels 0 and 1 at batch 1); DC_ATTN_PP=0 disables it,
+// 2 takes it wherever the slab fits (tests); a forced DC_ATTN_CFG bypasses it.
+bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, float* ws,
+                   long ws_bytes, hipStream_t st) {
+  const char* env = getenv("DC_ATTN_PP");   // read per launch (host side, once per captured graph node)
+  if (!ws || (env && atoi(env) == 0) || getenv("DC_ATTN_CFG")) return false;
+  const bool forced = env && atoi(env) == 2;
+  const long units = (long)((t + PP_QPB - 1) / PP_QPB) * heads * nb;
+  const int ntile = (t + 63) / 64;
+  const long G = device_cus();
+  const long U = units * ntile;
+  if (!forced && U < 16 * G) return false;
+  if (units > kAttnCounterBytes / 4) return false;
+  const long g = min(G, U);
+  const int spb = (int)(((U + g - 1) / g + ntile - 1) / ntile + 1);
+  if (g * spb * 8 * 34 * 64L * 4 > ws_bytes - kAttnCounterBytes) return false;
+  AttnSK sk;
+  sk.slab = ws;
+  sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + (ws_bytes - kAttnCounterBytes));
+  sk.U = U;
+  sk.G = (int)g;
+  sk.spb = spb;
+  hipLaunchKernelGGL(attn_fwd_pp_kernel, dim3((unsigned)g), dim3(512), 0, st, qkv, ld, t, heads, o, ldo, lse, sk);
+  return true;
+}
 }  // namespace
 
 extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse,
@@ -1180,7 +1490,8 @@ extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, vo
   if (ld % 8 || ldo % 8 || ld < 3 * heads * 64 || ldo < heads * 64) return DC_ERR_ALIGN;
   const bf16* q = (const bf16*)qkv;
   hipStream_t st = (hipStream_t)stream;
-  if (launch_fwd_sk(q, ld, t, heads, nb, (bf16*)o, ldo, lse, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st)) {
+  if (launch_fwd_sk(q, ld, t, heads, nb, (bf16*)o, ldo, lse, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st) ||
+      launch_fwd_pp(q, ld, t, heads, nb, (bf16*)o, ldo, lse, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st)) {
     DC_CHECK_LAUNCH();
     return DC_OK;
   }

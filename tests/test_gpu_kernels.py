@@ -505,6 +505,35 @@ def test_attention_fwd_stream_k(ctx, n, t, heads, monkeypatch):
     assert rel(outs["2"][1], lse_ref) < 1e-4
 
 
+@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (1, 65, 2), (1, 300, 2), (3, 257, 2), (2, 1000, 3), (1, 1728, 10),
+                                       (1, 6912, 5)])
+def test_attention_fwd_pingpong(ctx, n, t, heads, monkeypatch):
+    """Ping-pong forward (8-wave blocks, halves one segment apart, stream-K over 256-query blocks; DC_ATTN_PP=2
+    forces it at every shape): bit-identical on repeat, equal to the one-barrier-per-tile kernels up to
+    summation order, and against fp32 SDPA / logsumexp.  (1, 65, 2): a one-key last tile; (3, 257, 2): a
+    one-query last block; (1, 6912, 5) / (1, 1728, 10): the UNet level-0 / level-1 shapes of the default policy."""
+    from depth_completion_amd import ops
+    C = heads * 64
+    qkv = rnd(n, t, 3 * C, seed=35).to(torch.bfloat16).float()
+    q, k, v = qkv.split(C, -1)
+    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
+    ref = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
+    lse_ref = torch.logsumexp(torch.einsum("nhqd,nhkd->nhqk", sh(q), sh(k)) / 8, -1)
+    qkv_b = qkv.to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
+    outs = {}
+    for mode in ("0", "2", "2b"):
+        monkeypatch.setenv("DC_ATTN_PP", mode[0])
+        ob = torch.zeros(n * t, C, dtype=torch.bfloat16, device=dev)
+        lse = torch.zeros(n, heads, t, device=dev)
+        ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
+        torch.cuda.synchronize()
+        outs[mode] = (ob, lse)
+    assert torch.equal(outs["2"][0], outs["2b"][0]) and torch.equal(outs["2"][1], outs["2b"][1])
+    assert rel(outs["2"][0], outs["0"][0]) < 5e-3
+    assert rel(outs["2"][0].view(n, t, C), ref) < 1e-2
+    assert rel(outs["2"][1], lse_ref) < 1e-4
+
+
 @pytest.mark.parametrize("n,t,heads", [(1, 300, 2), (2, 1000, 3), (1, 6912, 5)])
 def test_attention_bwd_stream_k(ctx, n, t, heads, monkeypatch):
     """Stream-K backward (equal ranges of the flattened (block, tile) space over 2 blocks per CU, partials
