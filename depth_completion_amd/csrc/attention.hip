@@ -625,13 +625,26 @@ struct PpState {
 // LDS reads by asm in consumption order, at most 12 in flight (lgkmcnt counts to 15), each group waited
 // for just before its MFMAs: K rows of key half 0 / 1, then the V^T k-slices 0..3 (2 fragments each).
 template <bool QK, bool PV, int KST, int VST>
-__device__ __forceinline__ void pp_mfma(PpState& w, const unsigned (&ka)[2][4], const unsigned (&va)[4][2][2]) {
+__device__ __forceinline__ void pp_mfma(PpState& w, const unsigned (&ka)[4], const unsigned (&va)[2][2]) {
+  // key half b adds 4096 B and a V^T k-slice 2048 B (the swizzle depends on row bits 1-3 only): immediates
   constexpr int KI = KST * PP_STAGE;
   constexpr int VI = VST * PP_STAGE + TILE_B;
   bf16x8 kf[2][4], vf[4][2];
-  auto vread = [&](int s) __attribute__((always_inline)) {
-#pragma unroll
-    for (int db = 0; db < 2; ++db) vf[s][db] = trans_frag_nw<VI>(va[s][db][0], va[s][db][1]);
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  auto vread = [&](auto S) __attribute__((always_inline)) {
+    constexpr int s = decltype(S)::value;
+    vf[s][0] = trans_frag_nw<VI + 2048 * s>(va[0][0], va[0][1]);
+    vf[s][1] = trans_frag_nw<VI + 2048 * s>(va[1][0], va[1][1]);
+  };
+  auto kread = [&](auto B) __attribute__((always_inline)) {
+    constexpr int b = decltype(B)::value;
+    kf[b][0] = ds_read128_nw<KI + 4096 * b>(ka[0]);
+    kf[b][1] = ds_read128_nw<KI + 4096 * b>(ka[1]);
+    kf[b][2] = ds_read128_nw<KI + 4096 * b>(ka[2]);
+    kf[b][3] = ds_read128_nw<KI + 4096 * b>(ka[3]);
   };
   auto qk = [&](int b) __attribute__((always_inline)) {
 #pragma unroll
@@ -645,33 +658,31 @@ __device__ __forceinline__ void pp_mfma(PpState& w, const unsigned (&ka)[2][4], 
       w.oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], w.pf[s], w.oacc[db], 0, 0, 0);
   };
   if constexpr (QK) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) kf[b][s] = ds_read128_nw<KI>(ka[b][s]);
+    kread(I0{});
+    kread(I1{});
   }
   if constexpr (QK && PV) {
-    vread(0);                                                     // K0 K1 V0 in flight
+    vread(I0{});                                                  // K0 K1 V0 in flight
     lgkm_wait<8>(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
     qk(0);
-    vread(1);                                                     // K1 V0 V1
+    vread(I1{});                                                  // K1 V0 V1
     lgkm_wait<8>(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
     qk(1);
-    vread(2);                                                     // V0 V1 V2
+    vread(I2{});                                                  // V0 V1 V2
   } else if constexpr (QK) {
     lgkm_wait<4>(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
     qk(0);
     lgkm_wait<0>(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
     qk(1);
   } else {
-    vread(0);
-    vread(1);
-    vread(2);
+    vread(I0{});
+    vread(I1{});
+    vread(I2{});
   }
   if constexpr (PV) {
     lgkm_wait<8>(vf[0][0], vf[0][1]);
     pv(0);
-    vread(3);                                                     // V1 V2 V3
+    vread(I3{});                                                  // V1 V2 V3
     lgkm_wait<8>(vf[1][0], vf[1][1]);
     pv(1);
     lgkm_wait<4>(vf[2][0], vf[2][1]);
@@ -727,6 +738,80 @@ __device__ __forceinline__ void pp_softmax(PpState& w, int kt, int T, int hh) {
   for (int s = 0; s < 4; ++s) w.pf[s] = acc_to_frag(w.sacc[s >> 1], s & 1);
 }
 
+// The segment schedule shared by the ping-pong kernels (attn_fwd_pp_kernel, attn_bwd_dq_pp_kernel).  A walk
+// segment of nt key tiles is nt * NB steps (NB parts per tile).  Segment s: half A runs the MFMA phase of step
+// s / 2 when s is even and the VALU phase of step (s - 1) / 2 when s is odd; half B the same one segment later.
+// F::mfma<KST, VST, P, PP>(j) is the MFMA phase of step j (its tile in ring stage KST, part P) with the
+// dependent products of step j - 1 (stage VST, part PP); j == nt NB: only step j - 1's part.  F::valu(j) is the
+// VALU phase of step j.  Ring: tile u + 2 is issued (issue(u), stage u % PP_S) in the segment of A's first
+// step of tile u, after B's last read of tile u - 2 (its dependent products of the last step of tile u - 2,
+// one segment earlier), and waited for before A's first step of tile u + 2; NV = LDS-DMA instructions per tile
+// of the wave (vmcnt of one younger tile).
+template <int NV, int NB, typename F, typename I>
+__device__ __forceinline__ void pp_drive(F& f, I&& issue, int nt, int half) {
+  issue(0);
+  if (nt > 1) {
+    issue(1);
+    vm_wait_n<NV>();
+  } else {
+    vm_wait_n<0>();
+  }
+  __syncthreads();
+  const int nst = nt * NB;
+  const int nseg = 2 * nst + 2;
+  auto segment = [&](int s, auto CC) __attribute__((always_inline)) {
+    constexpr int c = decltype(CC)::value;   // s % (8 NB): ring stages and parts are compile-time per copy
+    constexpr int JA = c / 2, JB = (c - 1) / 2;               // A's / B's step mod 4 NB (MFMA copies)
+    constexpr int JAP = (JA + 4 * NB - 1) % (4 * NB), JBP = (JB + 4 * NB - 1) % (4 * NB);
+    if (s >= nseg) return;
+    if constexpr ((c & 1) == 0 && JA % NB == 0) {
+      if (s / (2 * NB) + 2 < nt) issue(s / (2 * NB) + 2);
+    }
+    if (half == 0) {
+      if constexpr ((c & 1) == 0) f.template mfma<JA / NB, JAP / NB, JA % NB, JAP % NB>(s / 2);
+      else if ((s - 1) / 2 < nst) f.valu((s - 1) / 2);
+    } else {
+      if constexpr ((c & 1) == 1) f.template mfma<JB / NB, JBP / NB, JB % NB, JBP % NB>((s - 1) / 2);
+      else if (s >= 2) f.valu((s - 2) / 2);
+    }
+    if constexpr ((c & 1) == 1 && ((c + 1) / 2) % NB == 0) {
+      // tile (s + 1) / (2 NB), A's next step, landed; the tile after it may stay in flight
+      if ((s + 1) / (2 * NB) + 1 < nt) vm_wait_n<NV>();
+      else vm_wait_n<0>();
+    }
+    __syncthreads();
+  };
+  auto run8 = [&](int s0, auto OFF) __attribute__((always_inline)) {
+    constexpr int o = decltype(OFF)::value;
+    segment(s0 + o, std::integral_constant<int, o>{});
+    segment(s0 + o + 1, std::integral_constant<int, o + 1>{});
+    segment(s0 + o + 2, std::integral_constant<int, o + 2>{});
+    segment(s0 + o + 3, std::integral_constant<int, o + 3>{});
+    segment(s0 + o + 4, std::integral_constant<int, o + 4>{});
+    segment(s0 + o + 5, std::integral_constant<int, o + 5>{});
+    segment(s0 + o + 6, std::integral_constant<int, o + 6>{});
+    segment(s0 + o + 7, std::integral_constant<int, o + 7>{});
+  };
+  for (int s0 = 0; s0 < nseg; s0 += 8 * NB) {
+    run8(s0, std::integral_constant<int, 0>{});
+    if constexpr (NB == 2) run8(s0, std::integral_constant<int, 8>{});
+  }
+}
+
+struct FwdPpOps {
+  PpState& w;
+  const unsigned (&ka)[4];
+  const unsigned (&va)[2][2];
+  int nt, t0, T, hh;
+  template <int KST, int VST, int P, int PP>
+  __device__ __forceinline__ void mfma(int t) {
+    if (t == 0) pp_mfma<true, false, KST, VST>(w, ka, va);
+    else if (t < nt) pp_mfma<true, true, KST, VST>(w, ka, va);
+    else pp_mfma<false, true, KST, VST>(w, ka, va);
+  }
+  __device__ __forceinline__ void valu(int t) { pp_softmax(w, t0 + t, T, hh); }
+};
+
 __device__ __forceinline__ void fwd_pp_segment(char* smem, const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo,
                                                float* lse, int qbk, int h, int n, int t0, int nt, const AttnSK& sk,
                                                long bi, int seg, bool whole) {
@@ -757,78 +842,17 @@ __device__ __forceinline__ void fwd_pp_segment(char* smem, const bf16* qkv, int 
     dma.issue(rv, st + TILE_B, (t0 + u) * 64, T, ld, threadIdx.x);
   };
   const unsigned sb = lds_addr(smem);
-  unsigned ka[2][4], va[4][2][2];
+  unsigned ka[4], va[2][2];
 #pragma unroll
-  for (int b = 0; b < 2; ++b)
+  for (int s = 0; s < 4; ++s) ka[s] = sb + row_off(lane & 31, 2 * s + hh);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) ka[b][s] = sb + row_off(32 * b + (lane & 31), 2 * s + hh);
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      const TrOff t = tr_off(16 * s, 32 * db, lane);
-      va[s][db][0] = sb + t.lo;
-      va[s][db][1] = sb + t.hi;
-    }
-  // prologue: tiles 0 and 1 in flight, tile 0 landed before segment 0
-  issue(0);
-  if (nt > 1) {
-    issue(1);
-    vm_wait_n<2>();
-  } else {
-    vm_wait_n<0>();
+  for (int db = 0; db < 2; ++db) {
+    const TrOff t = tr_off(0, 32 * db, lane);
+    va[db][0] = sb + t.lo;
+    va[db][1] = sb + t.hi;
   }
-  __syncthreads();
-
-  // segment s: half A is in its MFMA phase of tile s / 2 when s is even and in its softmax of tile (s - 1) / 2
-  // when s is odd; half B the same one segment later.  Ring: tile u + 2 is issued in segment 2u (its stage
-  // was last read by B's PV of tile u - 2 in segment 2u - 1) and waited for at the end of segment 2u + 3.
-  const int nseg = 2 * nt + 2;
-  auto segment = [&](int s, auto CC) __attribute__((always_inline)) {
-    constexpr int c = decltype(CC)::value;   // s % 8: the ring stages are compile-time per copy
-    if (s >= nseg) return;
-    if constexpr ((c & 1) == 0) {
-      if (s / 2 + 2 < nt) issue(s / 2 + 2);
-    }
-    if (half == 0) {
-      if constexpr ((c & 1) == 0) {
-        constexpr int KST = (c / 2) % PP_S, VST = (c / 2 + PP_S - 1) % PP_S;
-        const int t = s / 2;
-        if (t == 0) pp_mfma<true, false, KST, VST>(w, ka, va);
-        else if (t < nt) pp_mfma<true, true, KST, VST>(w, ka, va);
-        else pp_mfma<false, true, KST, VST>(w, ka, va);
-      } else {
-        const int t = (s - 1) / 2;
-        if (t < nt) pp_softmax(w, t0 + t, T, hh);
-      }
-    } else {
-      if constexpr ((c & 1) == 1) {
-        constexpr int KST = ((c - 1) / 2) % PP_S, VST = ((c - 1) / 2 + PP_S - 1) % PP_S;
-        const int t = (s - 1) / 2;
-        if (t == 0) pp_mfma<true, false, KST, VST>(w, ka, va);
-        else if (t < nt) pp_mfma<true, true, KST, VST>(w, ka, va);
-        else pp_mfma<false, true, KST, VST>(w, ka, va);
-      } else {
-        if (s >= 2) pp_softmax(w, t0 + (s - 2) / 2, T, hh);
-      }
-    }
-    if constexpr ((c & 1) == 1) {
-      // tile u = (s + 1) / 2 (A's next QK) landed; tile u + 1, issued in segment s - 1, may stay in flight
-      if ((s + 1) / 2 + 1 < nt) vm_wait_n<2>();
-      else vm_wait_n<0>();
-    }
-    __syncthreads();
-  };
-  for (int s0 = 0; s0 < nseg; s0 += 8) {
-    segment(s0, std::integral_constant<int, 0>{});
-    segment(s0 + 1, std::integral_constant<int, 1>{});
-    segment(s0 + 2, std::integral_constant<int, 2>{});
-    segment(s0 + 3, std::integral_constant<int, 3>{});
-    segment(s0 + 4, std::integral_constant<int, 4>{});
-    segment(s0 + 5, std::integral_constant<int, 5>{});
-    segment(s0 + 6, std::integral_constant<int, 6>{});
-    segment(s0 + 7, std::integral_constant<int, 7>{});
-  }
+  FwdPpOps ops{w, ka, va, nt, t0, T, hh};
+  pp_drive<2, 1>(ops, issue, nt, half);
   float m = w.m, l = w.l + __shfl_xor(w.l, 32, 64);
   if (!whole) {   // query block shared with other blocks: merge (m, l, O) in block order
     float v[34];
@@ -1335,6 +1359,202 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
   }
 }
 
+
+// -------------------------------------------------------------------------------- dQ, ping-pong
+// pp_drive's schedule for dQ, two steps per key tile (32 keys each, to fit two waves' registers per SIMD):
+// 8-wave blocks, 32 queries per wave resident (Q, dO fragments, lse, delta), K / V tiles through the shared
+// ring.  MFMA phase of step j: S^T = K Q^T and dP^T = V dO^T of its 32 keys, dQ^T += K^T dS^T of step j - 1
+// (12 MFMAs); VALU phase: P = exp2(S log2e - lse), dS = P (dP - delta), tail keys masked, dS packed to bf16.
+// Stream-K over (256-query block, key tile), partial dQ summed in block order by the last arriver
+// (sk_handoff); delta published by the segment that starts at key 0 (the dK/dV kernel runs next).
+struct DqPpState {
+  bf16x8 qf[4], df[4];
+  f32x16 sacc, dpacc, dq[2];
+  bf16x8 sf[2];   // dS^T of the previous step by k-slice
+  float lse2, del;
+};
+
+// LDS reads by asm in consumption order, at most 12 in flight: K rows / V rows of the step's key half (tile
+// stage KST, half P), then the K^T fragments of step j - 1 (stage VST, half PP) by k-slice.  A key half adds
+// 32 rows (4096 B), a k-slice 16 rows (2048 B); the swizzle depends on row bits 1-3 only, so both offsets are
+// immediates on 4 + 4 per-lane base addresses.
+template <bool QK, bool DQ, int KST, int VST, int P, int PP>
+__device__ __forceinline__ void dqpp_mfma(DqPpState& w, const unsigned (&ka)[4], const unsigned (&ta)[2][2]) {
+  constexpr int KI = KST * PP_STAGE + 4096 * P, VI = KI + TILE_B, TI = VST * PP_STAGE + 4096 * PP;
+  bf16x8 kf[4], vf[4], fq[2][2];
+  auto rk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[s] = ds_read128_nw<KI>(ka[s]);
+  };
+  auto rv = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) vf[s] = ds_read128_nw<VI>(ka[s]);
+  };
+  auto rt0 = [&]() __attribute__((always_inline)) {
+    fq[0][0] = trans_frag_nw<TI>(ta[0][0], ta[0][1]);
+    fq[0][1] = trans_frag_nw<TI>(ta[1][0], ta[1][1]);
+  };
+  auto rt1 = [&]() __attribute__((always_inline)) {
+    fq[1][0] = trans_frag_nw<TI + 2048>(ta[0][0], ta[0][1]);
+    fq[1][1] = trans_frag_nw<TI + 2048>(ta[1][0], ta[1][1]);
+  };
+  auto mk = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w.sacc[r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) w.sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], w.qf[s], w.sacc, 0, 0, 0);
+  };
+  auto mv = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w.dpacc[r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) w.dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s], w.df[s], w.dpacc, 0, 0, 0);
+  };
+  auto mt = [&](int s2) __attribute__((always_inline)) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+      w.dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq[s2][db], w.sf[s2], w.dq[db], 0, 0, 0);
+  };
+  if constexpr (QK && DQ) {
+    rk(); rv(); rt0();
+    lgkm_wait<8>(kf[0], kf[1], kf[2], kf[3]); mk(); rt1();
+    lgkm_wait<8>(vf[0], vf[1], vf[2], vf[3]); mv();
+    lgkm_wait<4>(fq[0][0], fq[0][1]); mt(0);
+    lgkm_wait<0>(fq[1][0], fq[1][1]); mt(1);
+  } else if constexpr (QK) {
+    rk(); rv();
+    lgkm_wait<4>(kf[0], kf[1], kf[2], kf[3]); mk();
+    lgkm_wait<0>(vf[0], vf[1], vf[2], vf[3]); mv();
+  } else {
+    rt0(); rt1();
+    lgkm_wait<4>(fq[0][0], fq[0][1]); mt(0);
+    lgkm_wait<0>(fq[1][0], fq[1][1]); mt(1);
+  }
+}
+
+struct DqPpOps {
+  DqPpState& w;
+  const unsigned (&ka)[4];
+  const unsigned (&ta)[2][2];
+  int nst, t0, T, hh;
+  template <int KST, int VST, int P, int PP>
+  __device__ __forceinline__ void mfma(int j) {
+    if (j == 0) dqpp_mfma<true, false, KST, VST, P, PP>(w, ka, ta);
+    else if (j < nst) dqpp_mfma<true, true, KST, VST, P, PP>(w, ka, ta);
+    else dqpp_mfma<false, true, KST, VST, P, PP>(w, ka, ta);
+  }
+  __device__ __forceinline__ void valu(int j) {
+    const int k0 = (t0 + (j >> 1)) * 64 + 32 * (j & 1);   // first key of the step
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pv = fast_exp2(fmaf(w.sacc[r], LOG2E, -w.lse2));
+      w.sacc[r] = pv * (w.dpacc[r] - w.del);   // dS^T
+    }
+    if (k0 + 32 > T) {  // keys beyond T exist only in the last tile
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (k0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) w.sacc[r] = 0.0f;
+    }
+    w.sf[0] = acc_to_frag(w.sacc, 0);
+    w.sf[1] = acc_to_frag(w.sacc, 1);
+  }
+};
+
+__device__ __forceinline__ void dq_pp_segment(char* smem, const bf16* qkv, int ld, const bf16* o, int ldo,
+                                              const bf16* dout, int lddo, const float* lse, float* delta, int T,
+                                              int heads, bf16* dqkv, int ldd, int qbk, int h, int n, int t0, int nt,
+                                              const AttnSK& sk, long bi, int seg, bool whole) {
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = threadIdx.x >> 6;
+  const int half = __builtin_amdgcn_readfirstlane(wid >> 2);
+  const int C = heads * 64;
+  const bf16* base = qkv + (long)n * T * ld;
+  const int my_q = qbk * PP_QPB + wid * 32 + (lane & 31);
+  const bool qok = my_q < T;
+  DqPpState w;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    w.qf[s] = load_row8(base + (long)my_q * ld + h * 64 + 16 * s + 8 * hh, qok, 0.125f);
+    w.df[s] = load_row8(dout + ((long)n * T + my_q) * lddo + h * 64 + 16 * s + 8 * hh, qok, 1.0f);
+  }
+  w.lse2 = qok ? lse[((long)n * heads + h) * T + my_q] * LOG2E : INFINITY;
+  // delta = sum_d dO * O (fp32, fixed order), as dq_segment
+  float my_del = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const bf16x8 of = load_row8(o + ((long)n * T + my_q) * ldo + h * 64 + 16 * s + 8 * hh, qok, 1.0f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) my_del = fmaf((float)w.df[s][j], (float)of[j], my_del);
+  }
+  my_del += __shfl_xor(my_del, 32, 64);
+  w.del = my_del;
+  if (qok && hh == 0 && t0 == 0) delta[((long)n * heads + h) * T + my_q] = my_del;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w.dq[db][r] = 0.0f;
+
+  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
+  const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
+  TileDma<512> dma;
+  dma.init(threadIdx.x, ld);
+  auto issue = [&](int u) __attribute__((always_inline)) {
+    char* st = smem + (u % PP_S) * PP_STAGE;
+    dma.issue(rk, st, (t0 + u) * 64, T, ld, threadIdx.x);
+    dma.issue(rv, st + TILE_B, (t0 + u) * 64, T, ld, threadIdx.x);
+  };
+  const unsigned sb = lds_addr(smem);
+  unsigned ka[4], ta[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) ka[s] = sb + row_off(lane & 31, 2 * s + hh);
+#pragma unroll
+  for (int db = 0; db < 2; ++db) {
+    const TrOff t = tr_off(0, 32 * db, lane);
+    ta[db][0] = sb + t.lo;
+    ta[db][1] = sb + t.hi;
+  }
+  DqPpOps ops{w, ka, ta, 2 * nt, t0, T, hh};
+  pp_drive<2, 2>(ops, issue, nt, half);
+  if (!whole) {
+    float v[32];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[16 * db + r] = w.dq[db][r];
+    if (!sk_handoff<8, 32>(sk, smem, bi, (T + 63) / 64, seg, v)) return;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) w.dq[db][r] = v[16 * db + r];
+  }
+  if (qok) {
+    bf16* row = dqkv + ((long)n * T + my_q) * ldd + h * 64;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g2 = 0; g2 < 4; ++g2) {
+        bf16x4 a;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = (bf16)(w.dq[db][4 * g2 + e] * 0.125f);
+        *reinterpret_cast<bf16x4*>(row + 32 * db + 8 * g2 + 4 * hh) = a;
+      }
+  }
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_pp_kernel(
+    const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse, float* delta,
+    int T, int heads, bf16* dqkv, int ldd, AttnSK sk) {
+  __shared__ __attribute__((aligned(16))) char smem[PP_S * PP_STAGE];
+  const int ntk = (T + 63) / 64;
+  const int nqb = (T + PP_QPB - 1) / PP_QPB;
+  sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
+    const int qbk = (int)(bi % nqb);
+    const long nh = bi / nqb;
+    dq_pp_segment(smem, qkv, ld, o, ldo, dout, lddo, lse, delta, T, heads, dqkv, ldd, qbk, (int)(nh % heads),
+                  (int)(nh / heads), t0, cnt, sk, bi, seg, t0 == 0 && cnt == ntk);
+  });
+}
 }  // namespace
 
 namespace {
@@ -1383,11 +1603,12 @@ void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int 
 // launch, same stream) reads it -- no separate delta pass
 template <int QW, int KS>
 void launch_bwd(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
-                float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, hipStream_t st) {
+                float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, bool with_dq, hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
   const AttnSK none{};
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, o, ldo, dout, lddo,
-                     lse, delta, t, heads, dqkv, ldd, none);
+  if (with_dq)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, o, ldo, dout,
+                       lddo, lse, delta, t, heads, dqkv, ldd, none);
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse,
                      delta, t, heads, dqkv, ldd, none);
 }
@@ -1432,11 +1653,12 @@ bool sk_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env
 
 bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
                    float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes,
-                   hipStream_t st) {
+                   bool with_dq, hipStream_t st) {
   AttnSK sk;
   if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK", sk)) return false;
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, o, ldo, dout,
-                     lddo, lse, delta, t, heads, dqkv, ldd, sk);
+  if (with_dq)
+    hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, o, ldo, dout,
+                       lddo, lse, delta, t, heads, dqkv, ldd, sk);
   hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout, lddo,
                      lse, delta, t, heads, dqkv, ldd, sk);
   return true;
@@ -1456,12 +1678,10 @@ bool launch_fwd_sk(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, i
   return true;
 }
 
-// Ping-pong forward (attn_fwd_pp_kernel): one 8-wave block per CU, stream-K over (256-query block, key tile).
-// Default wherever every block gets >= 16 key tiles (UNet levels 0 and 1 at batch 1); DC_ATTN_PP=0 disables it,
-// 2 takes it wherever the slab fits (tests); a forced DC_ATTN_CFG bypasses it.
-bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, float* ws,
-                   long ws_bytes, hipStream_t st) {
-  const char* env = getenv("DC_ATTN_PP");   // read per launch (host side, once per captured graph node)
+// stream-K plan of the 8-wave ping-pong kernels over (256-query block, key tile): one block per CU; NV fp32
+// partial values per lane and slab slot; false when it does not apply (env: "0" off, "2" wherever it fits)
+bool pp_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env_name, int nv, AttnSK& sk) {
+  const char* env = getenv(env_name);   // read per launch (host side, once per captured graph node)
   if (!ws || (env && atoi(env) == 0) || getenv("DC_ATTN_CFG")) return false;
   const bool forced = env && atoi(env) == 2;
   const long units = (long)((t + PP_QPB - 1) / PP_QPB) * heads * nb;
@@ -1472,14 +1692,33 @@ bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, i
   if (units > kAttnCounterBytes / 4) return false;
   const long g = min(G, U);
   const int spb = (int)(((U + g - 1) / g + ntile - 1) / ntile + 1);
-  if (g * spb * 8 * 34 * 64L * 4 > ws_bytes - kAttnCounterBytes) return false;
-  AttnSK sk;
+  if (g * spb * 8 * nv * 64L * 4 > ws_bytes - kAttnCounterBytes) return false;
   sk.slab = ws;
   sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + (ws_bytes - kAttnCounterBytes));
   sk.U = U;
   sk.G = (int)g;
   sk.spb = spb;
-  hipLaunchKernelGGL(attn_fwd_pp_kernel, dim3((unsigned)g), dim3(512), 0, st, qkv, ld, t, heads, o, ldo, lse, sk);
+  return true;
+}
+
+// Ping-pong forward (attn_fwd_pp_kernel): one 8-wave block per CU, stream-K over (256-query block, key tile).
+// Default wherever every block gets >= 16 key tiles (UNet levels 0 and 1 at batch 1); DC_ATTN_PP=0 disables it,
+// 2 takes it wherever the slab fits (tests); a forced DC_ATTN_CFG bypasses it.
+bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, float* ws,
+                   long ws_bytes, hipStream_t st) {
+  AttnSK sk;
+  if (!pp_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_PP", 34, sk)) return false;
+  hipLaunchKernelGGL(attn_fwd_pp_kernel, dim3((unsigned)sk.G), dim3(512), 0, st, qkv, ld, t, heads, o, ldo, lse, sk);
+  return true;
+}
+
+// Ping-pong dQ (attn_bwd_dq_pp_kernel), same policy as the forward's; DC_ATTN_PP_DQ=0 disables it.
+bool launch_dq_pp(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
+                  float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
+  AttnSK sk;
+  if (!pp_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_PP_DQ", 32, sk)) return false;
+  hipLaunchKernelGGL(attn_bwd_dq_pp_kernel, dim3((unsigned)sk.G), dim3(512), 0, st, qkv, ld, o, ldo, dout, lddo, lse,
+                     delta, t, heads, dqkv, ldd, sk);
   return true;
 }
 }  // namespace
@@ -1516,15 +1755,17 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   const bf16* ob = (const bf16*)o;
   const bf16* d = (const bf16*)dout;
   bf16* g = (bf16*)dqkv;
-  if (launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws,
-                    ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st)) {
+  const long wsb = ws_bytes < (1LL << 40) ? (long)ws_bytes : 0;
+  // dQ first (it publishes delta for dK/dV): the ping-pong kernel where its policy applies
+  const bool dq_done = launch_dq_pp(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, st);
+  if (launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, !dq_done, st)) {
     DC_CHECK_LAUNCH();
     return DC_OK;
   }
   switch (attn_cfg(t, heads, nb, true)) {
-    case 0: launch_bwd<4, 1>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
-    case 1: launch_bwd<4, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
-    default: launch_bwd<2, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, st); break;
+    case 0: launch_bwd<4, 1>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, !dq_done, st); break;
+    case 1: launch_bwd<4, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, !dq_done, st); break;
+    default: launch_bwd<2, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, !dq_done, st); break;
   }
   DC_CHECK_LAUNCH();
   return DC_OK;

@@ -1,6 +1,7 @@
 """Attention fwd/bwd microbenchmark at the UNet shapes (GPU). DC_ATTN_CFG=<i> forces a block configuration.
 
-The forward is timed with the ping-pong kernel off and on (DC_ATTN_PP=0 / 1, alternating, `--reps` pairs)."""
+The forward / backward are timed with the ping-pong forward / dQ kernel off and on (DC_ATTN_PP, DC_ATTN_PP_DQ = 0 / 1,
+alternating, `--reps` pairs)."""
 import argparse
 import os
 import sys
@@ -51,6 +52,12 @@ for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (8, 6912, 5), (8,
         print(f"n={n} T={t} H={heads} {name}: {ms*1e3:.1f} us  {f/ms/1e9:.0f} TF/s  (all: "
               f"{' '.join(f'{x*1e3:.1f}' for x in res[mode])})", flush=True)
     if not args.no_bwd:
-        ms = timed(lambda: ops.attn_bwd(ctx, qkv, o, do, lse, n, t, heads, delta, dq))
-        print(f"n={n} T={t} H={heads} bwd: {ms*1e3:.1f} us  {3.5*f/ms/1e9:.0f} TF/s (algorithmic incl. recompute)",
-              flush=True)
+        rb = {"0": [], "1": []}
+        for _ in range(args.reps):
+            for mode in ("0", "1"):
+                os.environ["DC_ATTN_PP_DQ"] = mode
+                rb[mode].append(timed(lambda: ops.attn_bwd(ctx, qkv, o, do, lse, n, t, heads, delta, dq)))
+        for mode, name in (("0", "bwd"), ("1", "bwd-ppdq")):
+            ms = min(rb[mode])
+            print(f"n={n} T={t} H={heads} {name}: {ms*1e3:.1f} us  {3.5*f/ms/1e9:.0f} TF/s (algorithmic incl. recompute)"
+                  f"  (all: {' '.join(f'{x*1e3:.1f}' for x in rb[mode])})", flush=True)
