@@ -650,7 +650,8 @@ __device__ __forceinline__ void pp_mfma(PpState& w, const unsigned (&ka)[4], con
 #pragma unroll
     for (int r = 0; r < 16; ++r) w.sacc[b][r] = 0.0f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) w.sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[b][s], w.qf[s], w.sacc[b], 0, 0, 0);
+    for (int s = 0; s < 4; ++s)
+      w.sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[b][s], w.qf[s], w.sacc[b], 0, 0, 0);
   };
   auto pv = [&](int s) __attribute__((always_inline)) {
 #pragma unroll
@@ -1555,6 +1556,236 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
                   (int)(nh / heads), t0, cnt, sk, bi, seg, t0 == 0 && cnt == ntk);
   });
 }
+
+// ------------------------------------------------------------------------------ dK/dV, ping-pong
+// pp_drive's schedule for dK/dV, two 32-query steps per tile: 8-wave blocks, 32 keys per wave resident (K, V
+// fragments; dK^T, dV^T accumulators), Q / dO tiles through the shared ring, their lse / delta rows in a small
+// ring of their own.  MFMA phase of step j: S = Q K^T and dP = dO V^T of its 32 queries (8 MFMAs), dV^T += dO^T
+// P and dK^T += Q^T dS of step j - 1 (8 MFMAs); VALU phase: P = exp2(S log2e / 8 - lse log2e), dS = P (dP -
+// delta), both packed to bf16.  Queries beyond T have zero Q / dO / lse / delta rows, so they add nothing.
+// Stream-K over (256-key block, query tile), partial dK / dV summed in block order by the last arriver.
+constexpr int PPB_LSE = PP_S * PP_STAGE;   // [stage][lse 64 | delta 64] fp32 after the Q / dO ring
+
+struct DkdvPpState {
+  bf16x8 kf[4], vf[4];
+  f32x16 dk[2], dv[2];
+  f32x16 sp, dp;
+  bf16x8 pf[2], sf[2];   // P / dS of the previous step by k-slice
+};
+
+// LDS reads by asm in consumption order, at most 12 in flight: Q rows / dO rows of the step's query half (stage
+// KST, half P), then the dO^T and Q^T fragments of step j - 1 (stage VST, half PP) by k-slice
+template <bool QK, bool DKV, int KST, int VST, int P, int PP>
+__device__ __forceinline__ void dkdvpp_mfma(DkdvPpState& w, const unsigned (&qa)[4], const unsigned (&ta)[2][2]) {
+  constexpr int QI = KST * PP_STAGE + 4096 * P, DI = QI + TILE_B;
+  constexpr int TQ = VST * PP_STAGE + 4096 * PP, TD = TQ + TILE_B;
+  bf16x8 qr[4], dr[4], fv[2][2], fk[2][2];
+  auto rq = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qr[s] = ds_read128_nw<QI>(qa[s]);
+  };
+  auto rd = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) dr[s] = ds_read128_nw<DI>(qa[s]);
+  };
+  auto rfv = [&](auto S2) __attribute__((always_inline)) {
+    constexpr int s2 = decltype(S2)::value;
+    fv[s2][0] = trans_frag_nw<TD + 2048 * s2>(ta[0][0], ta[0][1]);
+    fv[s2][1] = trans_frag_nw<TD + 2048 * s2>(ta[1][0], ta[1][1]);
+  };
+  auto rfk = [&](auto S2) __attribute__((always_inline)) {
+    constexpr int s2 = decltype(S2)::value;
+    fk[s2][0] = trans_frag_nw<TQ + 2048 * s2>(ta[0][0], ta[0][1]);
+    fk[s2][1] = trans_frag_nw<TQ + 2048 * s2>(ta[1][0], ta[1][1]);
+  };
+  auto ms = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w.sp[r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) w.sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr[s], w.kf[s], w.sp, 0, 0, 0);
+  };
+  auto md = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) w.dp[r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) w.dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr[s], w.vf[s], w.dp, 0, 0, 0);
+  };
+  auto mdv = [&](int s2) __attribute__((always_inline)) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+      w.dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fv[s2][db], w.pf[s2], w.dv[db], 0, 0, 0);
+  };
+  auto mdk = [&](int s2) __attribute__((always_inline)) {
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+      w.dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk[s2][db], w.sf[s2], w.dk[db], 0, 0, 0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if constexpr (QK && DKV) {
+    rq(); rd(); rfv(I0{});
+    lgkm_wait<8>(qr[0], qr[1], qr[2], qr[3]); ms(); rfk(I0{});
+    lgkm_wait<8>(dr[0], dr[1], dr[2], dr[3]); md(); rfv(I1{});
+    lgkm_wait<8>(fv[0][0], fv[0][1]); mdv(0); rfk(I1{});
+    lgkm_wait<8>(fk[0][0], fk[0][1]); mdk(0);
+    lgkm_wait<4>(fv[1][0], fv[1][1]); mdv(1);
+    lgkm_wait<0>(fk[1][0], fk[1][1]); mdk(1);
+  } else if constexpr (QK) {
+    rq(); rd();
+    lgkm_wait<4>(qr[0], qr[1], qr[2], qr[3]); ms();
+    lgkm_wait<0>(dr[0], dr[1], dr[2], dr[3]); md();
+  } else {
+    rfv(I0{}); rfk(I0{}); rfv(I1{});
+    lgkm_wait<8>(fv[0][0], fv[0][1]); mdv(0); rfk(I1{});
+    lgkm_wait<8>(fk[0][0], fk[0][1]); mdk(0);
+    lgkm_wait<4>(fv[1][0], fv[1][1]); mdv(1);
+    lgkm_wait<0>(fk[1][0], fk[1][1]); mdk(1);
+  }
+}
+
+struct DkdvPpOps {
+  DkdvPpState& w;
+  const unsigned (&qa)[4];
+  const unsigned (&ta)[2][2];
+  const char* lsb;   // lse / delta ring
+  int nst, hh;
+  template <int KST, int VST, int P, int PP>
+  __device__ __forceinline__ void mfma(int j) {
+    if (j == 0) dkdvpp_mfma<true, false, KST, VST, P, PP>(w, qa, ta);
+    else if (j < nst) dkdvpp_mfma<true, true, KST, VST, P, PP>(w, qa, ta);
+    else dkdvpp_mfma<false, true, KST, VST, P, PP>(w, qa, ta);
+  }
+  __device__ __forceinline__ void valu(int j) {
+    constexpr float L8 = LOG2E * 0.125f;
+    // accumulator element r holds query 32 (j & 1) + 8 (r >> 2) + 4 hh + (r & 3) of the tile
+    const float* ls = reinterpret_cast<const float*>(lsb + ((j >> 1) % PP_S) * 512) + 32 * (j & 1) + 4 * hh;
+    const float* dl = ls + 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + 8 * g);
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + 8 * g);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = fast_exp2(fmaf(w.sp[4 * g + e], L8, -l4[e] * LOG2E));
+        w.sp[4 * g + e] = pv;
+        w.dp[4 * g + e] = pv * (w.dp[4 * g + e] - d4[e]);
+      }
+    }
+    w.pf[0] = acc_to_frag(w.sp, 0);
+    w.pf[1] = acc_to_frag(w.sp, 1);
+    w.sf[0] = acc_to_frag(w.dp, 0);
+    w.sf[1] = acc_to_frag(w.dp, 1);
+  }
+};
+
+__device__ __forceinline__ void dkdv_pp_segment(char* smem, const bf16* qkv, int ld, const bf16* dout, int lddo,
+                                                const float* lse, const float* delta, int T, int heads, bf16* dqkv,
+                                                int ldd, int kb, int h, int n, int t0, int nt, const AttnSK& sk,
+                                                long bi, int seg, bool whole) {
+  const int lane = threadIdx.x & 63, hh = lane >> 5;
+  const int wid = threadIdx.x >> 6;
+  const int half = __builtin_amdgcn_readfirstlane(wid >> 2);
+  const int C = heads * 64;
+  const bf16* base = qkv + (long)n * T * ld;
+  const bf16* dob = dout + (long)n * T * lddo;
+  const int my_k = kb * PP_QPB + wid * 32 + (lane & 31);
+  const bool kok = my_k < T;
+  DkdvPpState w;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    w.kf[s] = load_row8(base + (long)my_k * ld + C + h * 64 + 16 * s + 8 * hh, kok, 1.0f);
+    w.vf[s] = load_row8(base + (long)my_k * ld + 2 * C + h * 64 + 16 * s + 8 * hh, kok, 1.0f);
+  }
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      w.dk[db][r] = 0.0f;
+      w.dv[db][r] = 0.0f;
+    }
+  const __amdgpu_buffer_rsrc_t rq = buf_rsrc(base + h * 64);
+  const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dob + h * 64);
+  const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lse + ((long)n * heads + h) * T);
+  const __amdgpu_buffer_rsrc_t rdl = buf_rsrc(delta + ((long)n * heads + h) * T);
+  TileDma<512> q_dma, d_dma;
+  q_dma.init(threadIdx.x, ld);
+  d_dma.init(threadIdx.x, lddo);
+  const int wv = __builtin_amdgcn_readfirstlane(wid);
+  char* lsb = smem + PPB_LSE;
+  auto issue = [&](int u) __attribute__((always_inline)) {
+    char* st = smem + (u % PP_S) * PP_STAGE;
+    const int r0 = (t0 + u) * 64;
+    q_dma.issue(rq, st, r0, T, ld, threadIdx.x);
+    d_dma.issue(rd, st + TILE_B, r0, T, lddo, threadIdx.x);
+    if (wv == 0) {  // lse / delta rows of the tile (rows >= T read 0)
+      const int soff = __builtin_amdgcn_readfirstlane(r0 * 4);
+      char* ls = lsb + (u % PP_S) * 512;
+      buf_load_lds4(rl, (DC_LDS char*)ls, r0 + lane < T ? lane * 4 : kOOB, soff);
+      buf_load_lds4(rdl, (DC_LDS char*)ls + 256, r0 + lane < T ? lane * 4 : kOOB, soff);
+    }
+  };
+  const unsigned sb = lds_addr(smem);
+  unsigned qa[4], ta[2][2];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qa[s] = sb + row_off(lane & 31, 2 * s + hh);
+#pragma unroll
+  for (int db = 0; db < 2; ++db) {
+    const TrOff t = tr_off(0, 32 * db, lane);
+    ta[db][0] = sb + t.lo;
+    ta[db][1] = sb + t.hi;
+  }
+  DkdvPpOps ops{w, qa, ta, lsb, 2 * nt, hh};
+  pp_drive<2, 2>(ops, issue, nt, half);   // (wave 0 has 4 instructions per tile: vmcnt(2) over-waits, safely)
+  if (!whole) {
+    float v[64];
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        v[16 * db + r] = w.dk[db][r];
+        v[32 + 16 * db + r] = w.dv[db][r];
+      }
+    if (!sk_handoff<8, 64>(sk, smem, bi, (T + 63) / 64, seg, v)) return;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        w.dk[db][r] = v[16 * db + r];
+        w.dv[db][r] = v[32 + 16 * db + r];
+      }
+  }
+  if (kok) {
+    bf16* row = dqkv + ((long)n * T + my_k) * ldd;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g2 = 0; g2 < 4; ++g2) {
+        bf16x4 a, b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          a[e] = (bf16)(w.dk[db][4 * g2 + e] * 0.125f);  // dK = dS^T (Q / 8)
+          b[e] = (bf16)w.dv[db][4 * g2 + e];
+        }
+        const int d = 32 * db + 8 * g2 + 4 * hh;
+        *reinterpret_cast<bf16x4*>(row + C + h * 64 + d) = a;
+        *reinterpret_cast<bf16x4*>(row + 2 * C + h * 64 + d) = b;
+      }
+  }
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_pp_kernel(
+    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
+    bf16* dqkv, int ldd, AttnSK sk) {
+  __shared__ __attribute__((aligned(16))) char smem[PPB_LSE + PP_S * 512];
+  const int ntq = (T + 63) / 64;
+  const int nkb = (T + PP_QPB - 1) / PP_QPB;
+  sk_walk(sk, ntq, [&](long bi, int t0, int cnt, int seg) {
+    const int kb = (int)(bi % nkb);
+    const long nh = bi / nkb;
+    dkdv_pp_segment(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, kb, (int)(nh % heads),
+                    (int)(nh / heads), t0, cnt, sk, bi, seg, t0 == 0 && cnt == ntq);
+  });
+}
 }  // namespace
 
 namespace {
@@ -1603,14 +1834,16 @@ void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int 
 // launch, same stream) reads it -- no separate delta pass
 template <int QW, int KS>
 void launch_bwd(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
-                float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, bool with_dq, hipStream_t st) {
+                float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, bool with_dq, bool with_dkdv,
+                hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
   const AttnSK none{};
   if (with_dq)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, o, ldo, dout,
                        lddo, lse, delta, t, heads, dqkv, ldd, none);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo, lse,
-                     delta, t, heads, dqkv, ldd, none);
+  if (with_dkdv)
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo,
+                       lse, delta, t, heads, dqkv, ldd, none);
 }
 
 int device_cus() {
@@ -1653,14 +1886,15 @@ bool sk_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env
 
 bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
                    float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes,
-                   bool with_dq, hipStream_t st) {
+                   bool with_dq, bool with_dkdv, hipStream_t st) {
   AttnSK sk;
   if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK", sk)) return false;
   if (with_dq)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, o, ldo, dout,
                        lddo, lse, delta, t, heads, dqkv, ldd, sk);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout, lddo,
-                     lse, delta, t, heads, dqkv, ldd, sk);
+  if (with_dkdv)
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout,
+                       lddo, lse, delta, t, heads, dqkv, ldd, sk);
   return true;
 }
 
@@ -1714,11 +1948,22 @@ bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, i
 
 // Ping-pong dQ (attn_bwd_dq_pp_kernel), same policy as the forward's; DC_ATTN_PP_DQ=0 disables it.
 bool launch_dq_pp(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
-                  float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
+                  float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes,
+                  hipStream_t st) {
   AttnSK sk;
   if (!pp_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_PP_DQ", 32, sk)) return false;
   hipLaunchKernelGGL(attn_bwd_dq_pp_kernel, dim3((unsigned)sk.G), dim3(512), 0, st, qkv, ld, o, ldo, dout, lddo, lse,
                      delta, t, heads, dqkv, ldd, sk);
+  return true;
+}
+
+// Ping-pong dK/dV (attn_bwd_dkdv_pp_kernel), same policy; DC_ATTN_PP_DKDV=0 disables it.
+bool launch_dkdv_pp(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
+                    int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
+  AttnSK sk;
+  if (!pp_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_PP_DKDV", 64, sk)) return false;
+  hipLaunchKernelGGL(attn_bwd_dkdv_pp_kernel, dim3((unsigned)sk.G), dim3(512), 0, st, qkv, ld, dout, lddo, lse, delta,
+                     t, heads, dqkv, ldd, sk);
   return true;
 }
 }  // namespace
@@ -1756,17 +2001,21 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   const bf16* d = (const bf16*)dout;
   bf16* g = (bf16*)dqkv;
   const long wsb = ws_bytes < (1LL << 40) ? (long)ws_bytes : 0;
-  // dQ first (it publishes delta for dK/dV): the ping-pong kernel where its policy applies
-  const bool dq_done = launch_dq_pp(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, st);
-  if (launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, !dq_done, st)) {
-    DC_CHECK_LAUNCH();
-    return DC_OK;
-  }
-  switch (attn_cfg(t, heads, nb, true)) {
-    case 0: launch_bwd<4, 1>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, !dq_done, st); break;
-    case 1: launch_bwd<4, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, !dq_done, st); break;
-    default: launch_bwd<2, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, !dq_done, st); break;
-  }
+  // dQ first (it publishes delta for dK/dV), then dK/dV: each by its ping-pong kernel where the policy applies,
+  // else by the stream-K or plain-grid kernels
+  auto legacy = [&](bool with_dq, bool with_dkdv) {
+    if (launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, with_dq, with_dkdv, st))
+      return;
+    const int cfg = attn_cfg(t, heads, nb, true);
+    if (cfg == 0)
+      launch_bwd<4, 1>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, with_dq, with_dkdv, st);
+    else if (cfg == 1)
+      launch_bwd<4, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, with_dq, with_dkdv, st);
+    else
+      launch_bwd<2, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, with_dq, with_dkdv, st);
+  };
+  if (!launch_dq_pp(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, st)) legacy(true, false);
+  if (!launch_dkdv_pp(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, st)) legacy(false, true);
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

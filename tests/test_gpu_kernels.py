@@ -568,6 +568,39 @@ def test_attention_dq_pingpong(ctx, n, t, heads, monkeypatch):
     assert rel(outs["2"][0].view(n, t, 3 * C)[..., :C], qkv.grad[..., :C]) < 2e-2
 
 
+@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (1, 65, 2), (1, 300, 2), (3, 257, 2), (2, 1000, 3), (1, 1728, 10),
+                                       (1, 6912, 5)])
+def test_attention_dkdv_pingpong(ctx, n, t, heads, monkeypatch):
+    """Ping-pong dK/dV (256 keys per block unit, two 32-query steps per tile; DC_ATTN_PP_DKDV=2 forces it): dK / dV
+    bit-identical on repeat and equal to the plain kernels up to summation order, dQ untouched (bitwise), and
+    against fp32 SDPA."""
+    from depth_completion_amd import ops
+    C = heads * 64
+    qkv = rnd(n, t, 3 * C, seed=38).to(torch.bfloat16).float().requires_grad_(True)
+    q, k, v = qkv.split(C, -1)
+    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
+    o = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
+    do = rnd(n, t, C, seed=39)
+    o.backward(do)
+    qkv_b = qkv.detach().to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
+    dob = do.to(torch.bfloat16).reshape(n * t, C)
+    ob = torch.empty(n * t, C, dtype=torch.bfloat16, device=dev)
+    lse = torch.empty(n, heads, t, device=dev)
+    ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
+    outs = {}
+    for mode in ("0", "2", "2b"):
+        monkeypatch.setenv("DC_ATTN_PP_DKDV", mode[0])
+        dq = torch.zeros_like(qkv_b)
+        delta = torch.empty(n, heads, t, device=dev)
+        ops.attn_bwd(ctx, qkv_b, ob, dob, lse, n, t, heads, delta, dq)
+        torch.cuda.synchronize()
+        outs[mode] = dq
+    assert torch.equal(outs["2"], outs["2b"])
+    assert torch.equal(outs["2"][:, :C], outs["0"][:, :C])
+    assert rel(outs["2"][:, C:], outs["0"][:, C:]) < 5e-3
+    assert rel(outs["2"].view(n, t, 3 * C)[..., C:], qkv.grad[..., C:]) < 2e-2
+
+
 @pytest.mark.parametrize("n,t,heads", [(1, 300, 2), (2, 1000, 3), (1, 6912, 5)])
 def test_attention_bwd_stream_k(ctx, n, t, heads, monkeypatch):
     """Stream-K backward (equal ranges of the flattened (block, tile) space over 2 blocks per CU, partials

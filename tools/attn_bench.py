@@ -1,6 +1,6 @@
 """Attention fwd/bwd microbenchmark at the UNet shapes (GPU). DC_ATTN_CFG=<i> forces a block configuration.
 
-The forward / backward are timed with the ping-pong forward / dQ kernel off and on (DC_ATTN_PP, DC_ATTN_PP_DQ = 0 / 1,
+The forward / backward are timed with the ping-pong forward / backward kernels off and on (DC_ATTN_PP, DC_ATTN_PP_DQ + DC_ATTN_PP_DKDV = 0 / 2 (forced wherever it fits),
 alternating, `--reps` pairs)."""
 import argparse
 import os
@@ -42,22 +42,23 @@ for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (8, 6912, 5), (8,
     dq = torch.empty_like(qkv)
     delta = torch.empty(n, heads, t, device=dev)
     f = 4.0 * n * t * t * 64 * heads
-    res = {"0": [], "1": []}
+    res = {"0": [], "2": []}
     for _ in range(args.reps):
-        for mode in ("0", "1"):
+        for mode in ("0", "2"):
             os.environ["DC_ATTN_PP"] = mode
             res[mode].append(timed(lambda: ops.attn_fwd(ctx, qkv, n, t, heads, o, lse)))
-    for mode, name in (("0", "fwd"), ("1", "fwd-pp")):
+    for mode, name in (("0", "fwd"), ("2", "fwd-pp")):
         ms = min(res[mode])
         print(f"n={n} T={t} H={heads} {name}: {ms*1e3:.1f} us  {f/ms/1e9:.0f} TF/s  (all: "
               f"{' '.join(f'{x*1e3:.1f}' for x in res[mode])})", flush=True)
     if not args.no_bwd:
-        rb = {"0": [], "1": []}
+        rb = {"0": [], "2": []}
         for _ in range(args.reps):
-            for mode in ("0", "1"):
+            for mode in ("0", "2"):
                 os.environ["DC_ATTN_PP_DQ"] = mode
+                os.environ["DC_ATTN_PP_DKDV"] = mode
                 rb[mode].append(timed(lambda: ops.attn_bwd(ctx, qkv, o, do, lse, n, t, heads, delta, dq)))
-        for mode, name in (("0", "bwd"), ("1", "bwd-ppdq")):
+        for mode, name in (("0", "bwd"), ("2", "bwd-pp")):
             ms = min(rb[mode])
             print(f"n={n} T={t} H={heads} {name}: {ms*1e3:.1f} us  {3.5*f/ms/1e9:.0f} TF/s (algorithmic incl. recompute)"
                   f"  (all: {' '.join(f'{x*1e3:.1f}' for x in rb[mode])})", flush=True)
