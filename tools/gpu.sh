@@ -16,6 +16,7 @@
 #   pmc | pmc8                 FETCH_SIZE, WRITE_SIZE, MFMA-busy passes over the conv kernels (eager C2 / C3, 4 steps)
 #   breakdown[=<batch>]        per-shape conv breakdown of one guided step (tools/conv_breakdown.py)
 #   stepprof                   per-shape conv time inside the graph-replayed step (tools/step_profile.py)
+#   pmcstep                    FETCH_SIZE / WRITE_SIZE / MFMA-busy passes over that same step (tools/pmc_step.py)
 #   py=<script args>           any repo python script (e.g. py=tools/gemm_one.py --m 6912)
 set -e
 tag=${1:?tag}
@@ -76,6 +77,16 @@ for step in "$@"; do
         python3 tools/step_profile.py --out "$out/descs.json" > "$out/stepprof.log" 2>&1
       python3 tools/step_profile.py --trace "$out/steptrace/run_kernel_trace.csv" --descs "$out/descs.json" \
         > "$out/step_shapes.txt" 2>&1 ;;
+    pmcstep)
+      # PMC passes over the graph-replayed step (one counter set per pass), then the per-step / per-launch record
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$out/pmcf" -o run --output-format csv -- \
+        python3 tools/step_profile.py --out "$out/descs.json" > "$out/pmcf.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$out/pmcw" -o run --output-format csv -- \
+        python3 tools/step_profile.py --out "$out/descs.json" > "$out/pmcw.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$out/pmcm" -o run \
+        --output-format csv -- python3 tools/step_profile.py --out "$out/descs.json" > "$out/pmcm.log" 2>&1
+      python3 tools/pmc_step.py "$out/pmcf/run_counter_collection.csv" "$out/pmcw/run_counter_collection.csv" \
+        "$out/pmcm/run_counter_collection.csv" "$out/descs.json" "$out/pmc_step.json" > "$out/pmc_step.log" 2>&1 ;;
     breakdown)
       timeout -k 10 300 python -u tools/conv_breakdown.py > "$out/conv_breakdown.txt" 2> "$out/conv_breakdown.err" ;;
     breakdown=*)
