@@ -221,9 +221,13 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
 
 
 def pmc_record(h, w, batch):
-    """Committed PMC pass for this latent shape (profiles/pmc_conv_gemm*.json), or None."""
+    """Committed PMC pass for this latent shape, or None: the pass over the graph-replayed step
+    (profiles/pmc_step*.json, tools/pmc_step.py: the population measure_conv_kernel times) before the older
+    eager-run passes (profiles/pmc_conv_gemm*.json)."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_conv_gemm*.json"))):
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_step*.json"))) + \
+        sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_conv_gemm*.json")))
+    for path in paths:
         with open(path) as f:
             rec = json.load(f)
         if rec.get("latent_shape") == [batch, h, w]:
@@ -430,6 +434,8 @@ def run_worker(args) -> None:
             t = pmc["traffic_bytes_per_launch"]
             roofline.update(traffic=round(t), traffic_unit="HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE)",
                             hbm_gbs=round(t / (avg_ms * 1e-3) / 1e9, 1), pmc_source=pmc["_file"])
+            if pmc.get("traffic_bytes_per_step") is not None:
+                roofline["traffic_per_step"] = round(pmc["traffic_bytes_per_step"])
             if pmc.get("mfma_util") is not None:
                 roofline["mfma_util"] = pmc["mfma_util"]
         line["roofline"] = roofline
