@@ -614,6 +614,31 @@ __device__ __forceinline__ bf16x8 ds_read128_nw(unsigned addr) {
   return r;
 }
 
+// max of three without the IEEE-mode canonicalisation fmaxf gets (one v_max_f32 x, x, x per operand): the
+// softmax inputs are MFMA results, NaN-free by construction
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// max over the two lanes of a row (lane l and l ^ 32) by v_permlane32_swap (no LDS round trip)
+__device__ __forceinline__ float rowmax_pair(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return max3_raw(__uint_as_float(r[0]), __uint_as_float(r[1]), x);
+}
+__device__ __forceinline__ float rowsum_pair(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// ring stage PP_S - 1 zeroed once per block before its first walk segment: the t = 0 MFMA phase multiplies that
+// stage (as tile -1) by zero operands, which must not meet NaN bit patterns in uninitialised LDS
+__device__ __forceinline__ void pp_zero_last_stage(char* smem) {
+  uint4* p = reinterpret_cast<uint4*>(smem + (PP_S - 1) * PP_STAGE);
+#pragma unroll
+  for (int i = threadIdx.x; i < PP_STAGE / 16; i += 512) p[i] = make_uint4(0, 0, 0, 0);
+}
+
 struct PpState {
   bf16x8 qf[4];
   f32x16 oacc[2], sacc[2];
@@ -693,27 +718,32 @@ __device__ __forceinline__ void pp_mfma(PpState& w, const unsigned (&ka)[4], con
   }
 }
 
-// VALU phase of key tile kt: masked tail, row max, lazy rescale of (O, l), exp2, fp32 row sum, P -> bf16
+// VALU phase of key tile kt: masked tail, row max, lazy rescale of (O, l), exp2, fp32 row sum, P -> bf16.
+// S stays read-only here (the weights go to temporaries): an in-place update makes S a value that differs
+// between the two halves' paths through a segment, and the merge then costs 32 register copies per segment.
 __device__ __forceinline__ void pp_softmax(PpState& w, int kt, int T, int hh) {
-  if ((kt + 1) * 64 > T) {
-    asm volatile("" ::: "memory");
+  const bool tail = (kt + 1) * 64 > T;   // keys beyond T exist only in the last tile
+  float mx;
+  if (!tail) {
+    float mx0 = max3_raw(w.sacc[0][0], w.sacc[0][1], w.sacc[0][2]);
+    float mx1 = max3_raw(w.sacc[1][0], w.sacc[1][1], w.sacc[1][2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) {
+      mx0 = max3_raw(mx0, w.sacc[0][r], w.sacc[0][r + 1]);
+      mx1 = max3_raw(mx1, w.sacc[1][r], w.sacc[1][r + 1]);
+    }
+    mx = max3_raw(max3_raw(mx0, mx1, w.sacc[0][15]), w.sacc[1][15], w.sacc[1][15]);
+  } else {
+    mx = -INFINITY;
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (key >= T) w.sacc[b][r] = -INFINITY;
+        mx = max3_raw(mx, key < T ? w.sacc[b][r] : -INFINITY, mx);
       }
   }
-  float mx0 = fmaxf(w.sacc[0][0], fmaxf(w.sacc[0][1], w.sacc[0][2]));
-  float mx1 = fmaxf(w.sacc[1][0], fmaxf(w.sacc[1][1], w.sacc[1][2]));
-#pragma unroll
-  for (int r = 3; r < 15; r += 2) {
-    mx0 = fmaxf(mx0, fmaxf(w.sacc[0][r], w.sacc[0][r + 1]));
-    mx1 = fmaxf(mx1, fmaxf(w.sacc[1][r], w.sacc[1][r + 1]));
-  }
-  float mx = fmaxf(fmaxf(mx0, w.sacc[0][15]), fmaxf(mx1, w.sacc[1][15]));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = rowmax_pair(mx);
   if (__any(mx > w.m + FWD_TAU)) {
     const float mnew = fmaxf(w.m, mx);
     const float alpha = fast_exp2((w.m - mnew) * LOG2E);
@@ -725,18 +755,28 @@ __device__ __forceinline__ void pp_softmax(PpState& w, int kt, int T, int hh) {
     w.m = mnew;
   }
   const float ml = w.m * LOG2E;
+  float p[2][16];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) p[b][r] = fast_exp2(fmaf(w.sacc[b][r], LOG2E, -ml));
+  if (tail) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) p[b][r] = 0.0f;
+  }
   float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float pv = fast_exp2(fmaf(w.sacc[b][r], LOG2E, -ml));
-      w.sacc[b][r] = pv;
-      ps[(b << 1) | (r & 1)] += pv;
-    }
+    for (int r = 0; r < 16; ++r) ps[(b << 1) | (r & 1)] += p[b][r];
   w.l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
 #pragma unroll
-  for (int s = 0; s < 4; ++s) w.pf[s] = acc_to_frag(w.sacc[s >> 1], s & 1);
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w.pf[s][j] = (bf16)p[s >> 1][8 * (s & 1) + j];
 }
 
 // The segment schedule shared by the ping-pong kernels (attn_fwd_pp_kernel, attn_bwd_dq_pp_kernel).  A walk
@@ -748,8 +788,8 @@ __device__ __forceinline__ void pp_softmax(PpState& w, int kt, int T, int hh) {
 // step of tile u, after B's last read of tile u - 2 (its dependent products of the last step of tile u - 2,
 // one segment earlier), and waited for before A's first step of tile u + 2; NV = LDS-DMA instructions per tile
 // of the wave (vmcnt of one younger tile).
-template <int NV, int NB, typename F, typename I>
-__device__ __forceinline__ void pp_drive(F& f, I&& issue, int nt, int half) {
+template <int NV, int NB, int H, typename F, typename I>
+__device__ __forceinline__ void pp_drive_half(F& f, I&& issue, int nt) {
   issue(0);
   if (nt > 1) {
     issue(1);
@@ -768,7 +808,7 @@ __device__ __forceinline__ void pp_drive(F& f, I&& issue, int nt, int half) {
     if constexpr ((c & 1) == 0 && JA % NB == 0) {
       if (s / (2 * NB) + 2 < nt) issue(s / (2 * NB) + 2);
     }
-    if (half == 0) {
+    if constexpr (H == 0) {
       if constexpr ((c & 1) == 0) f.template mfma<JA / NB, JAP / NB, JA % NB, JAP % NB>(s / 2);
       else if ((s - 1) / 2 < nst) f.valu((s - 1) / 2);
     } else {
@@ -799,17 +839,23 @@ __device__ __forceinline__ void pp_drive(F& f, I&& issue, int nt, int half) {
   }
 }
 
+// each half runs its own copy of the segment loop (same barrier sequence): no per-segment branch on the half, so
+// the values carried between a wave's phases have one definition per program point (no merge copies)
+template <int NV, int NB, typename F, typename I>
+__device__ __forceinline__ void pp_drive(F& f, I&& issue, int nt, int half) {
+  if (half == 0) pp_drive_half<NV, NB, 0>(f, issue, nt);
+  else pp_drive_half<NV, NB, 1>(f, issue, nt);
+}
+
 struct FwdPpOps {
   PpState& w;
   const unsigned (&ka)[4];
   const unsigned (&va)[2][2];
   int nt, t0, T, hh;
+  // one body for every tile: at t = 0 the PV part multiplies the zeroed ring stage by P = 0, at t = nt the QK
+  // part reads a stale stage whose S is never used (no per-tile variants: their merges cost register copies)
   template <int KST, int VST, int P, int PP>
-  __device__ __forceinline__ void mfma(int t) {
-    if (t == 0) pp_mfma<true, false, KST, VST>(w, ka, va);
-    else if (t < nt) pp_mfma<true, true, KST, VST>(w, ka, va);
-    else pp_mfma<false, true, KST, VST>(w, ka, va);
-  }
+  __device__ __forceinline__ void mfma(int) { pp_mfma<true, true, KST, VST>(w, ka, va); }
   __device__ __forceinline__ void valu(int t) { pp_softmax(w, t0 + t, T, hh); }
 };
 
@@ -832,6 +878,8 @@ __device__ __forceinline__ void fwd_pp_segment(char* smem, const bf16* qkv, int 
   for (int db = 0; db < 2; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) w.oacc[db][r] = 0.0f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) w.pf[s] = bf16x8{};   // tile -1's P: the first PV adds nothing
 
   const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
   const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
@@ -892,6 +940,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   __shared__ __attribute__((aligned(16))) char smem[PP_S * PP_STAGE];
   const int ntk = (T + 63) / 64;
   const int nqb = (T + PP_QPB - 1) / PP_QPB;
+  pp_zero_last_stage(smem);   // (made visible by the first walk segment's prologue barrier)
   sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
     const int qbk = (int)(bi % nqb);
     const long nh = bi / nqb;
@@ -1439,26 +1488,24 @@ struct DqPpOps {
   const unsigned (&ta)[2][2];
   int nst, t0, T, hh;
   template <int KST, int VST, int P, int PP>
-  __device__ __forceinline__ void mfma(int j) {
-    if (j == 0) dqpp_mfma<true, false, KST, VST, P, PP>(w, ka, ta);
-    else if (j < nst) dqpp_mfma<true, true, KST, VST, P, PP>(w, ka, ta);
-    else dqpp_mfma<false, true, KST, VST, P, PP>(w, ka, ta);
-  }
+  __device__ __forceinline__ void mfma(int) { dqpp_mfma<true, true, KST, VST, P, PP>(w, ka, ta); }   // as FwdPpOps
   __device__ __forceinline__ void valu(int j) {
     const int k0 = (t0 + (j >> 1)) * 64 + 32 * (j & 1);   // first key of the step
+    float ds[16];   // dS^T in temporaries (S / dP stay read-only: see pp_softmax)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float pv = fast_exp2(fmaf(w.sacc[r], LOG2E, -w.lse2));
-      w.sacc[r] = pv * (w.dpacc[r] - w.del);   // dS^T
+      ds[r] = pv * (w.dpacc[r] - w.del);
     }
     if (k0 + 32 > T) {  // keys beyond T exist only in the last tile
-      asm volatile("" ::: "memory");
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (k0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) w.sacc[r] = 0.0f;
+        if (k0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) ds[r] = 0.0f;
     }
-    w.sf[0] = acc_to_frag(w.sacc, 0);
-    w.sf[1] = acc_to_frag(w.sacc, 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w.sf[s2][e] = (bf16)ds[8 * s2 + e];
   }
 };
 
@@ -1490,6 +1537,8 @@ __device__ __forceinline__ void dq_pp_segment(char* smem, const bf16* qkv, int l
   }
   my_del += __shfl_xor(my_del, 32, 64);
   w.del = my_del;
+  w.sf[0] = bf16x8{};   // step -1's dS: the first dQ product adds nothing
+  w.sf[1] = bf16x8{};
   if (qok && hh == 0 && t0 == 0) delta[((long)n * heads + h) * T + my_q] = my_del;
 #pragma unroll
   for (int db = 0; db < 2; ++db)
@@ -1549,6 +1598,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   __shared__ __attribute__((aligned(16))) char smem[PP_S * PP_STAGE];
   const int ntk = (T + 63) / 64;
   const int nqb = (T + PP_QPB - 1) / PP_QPB;
+  pp_zero_last_stage(smem);   // (made visible by the first walk segment's prologue barrier)
   sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
     const int qbk = (int)(bi % nqb);
     const long nh = bi / nqb;
@@ -1650,31 +1700,30 @@ struct DkdvPpOps {
   const char* lsb;   // lse / delta ring
   int nst, hh;
   template <int KST, int VST, int P, int PP>
-  __device__ __forceinline__ void mfma(int j) {
-    if (j == 0) dkdvpp_mfma<true, false, KST, VST, P, PP>(w, qa, ta);
-    else if (j < nst) dkdvpp_mfma<true, true, KST, VST, P, PP>(w, qa, ta);
-    else dkdvpp_mfma<false, true, KST, VST, P, PP>(w, qa, ta);
-  }
+  __device__ __forceinline__ void mfma(int) { dkdvpp_mfma<true, true, KST, VST, P, PP>(w, qa, ta); }   // as FwdPpOps
   __device__ __forceinline__ void valu(int j) {
     constexpr float L8 = LOG2E * 0.125f;
     // accumulator element r holds query 32 (j & 1) + 8 (r >> 2) + 4 hh + (r & 3) of the tile
     const float* ls = reinterpret_cast<const float*>(lsb + ((j >> 1) % PP_S) * 512) + 32 * (j & 1) + 4 * hh;
     const float* dl = ls + 64;
+    float pv[16], ds[16];   // P / dS in temporaries (S / dP stay read-only: see pp_softmax)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + 8 * g);
       const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + 8 * g);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float pv = fast_exp2(fmaf(w.sp[4 * g + e], L8, -l4[e] * LOG2E));
-        w.sp[4 * g + e] = pv;
-        w.dp[4 * g + e] = pv * (w.dp[4 * g + e] - d4[e]);
+        pv[4 * g + e] = fast_exp2(fmaf(w.sp[4 * g + e], L8, -l4[e] * LOG2E));
+        ds[4 * g + e] = pv[4 * g + e] * (w.dp[4 * g + e] - d4[e]);
       }
     }
-    w.pf[0] = acc_to_frag(w.sp, 0);
-    w.pf[1] = acc_to_frag(w.sp, 1);
-    w.sf[0] = acc_to_frag(w.dp, 0);
-    w.sf[1] = acc_to_frag(w.dp, 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        w.pf[s2][e] = (bf16)pv[8 * s2 + e];
+        w.sf[s2][e] = (bf16)ds[8 * s2 + e];
+      }
   }
 };
 
@@ -1703,6 +1752,7 @@ __device__ __forceinline__ void dkdv_pp_segment(char* smem, const bf16* qkv, int
       w.dk[db][r] = 0.0f;
       w.dv[db][r] = 0.0f;
     }
+  w.pf[0] = w.pf[1] = w.sf[0] = w.sf[1] = bf16x8{};   // step -1's P / dS: the first products add nothing
   const __amdgpu_buffer_rsrc_t rq = buf_rsrc(base + h * 64);
   const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dob + h * 64);
   const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lse + ((long)n * heads + h) * T);
@@ -1779,6 +1829,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
   __shared__ __attribute__((aligned(16))) char smem[PPB_LSE + PP_S * 512];
   const int ntq = (T + 63) / 64;
   const int nkb = (T + PP_QPB - 1) / PP_QPB;
+  pp_zero_last_stage(smem);   // (made visible by the first walk segment's prologue barrier)
   sk_walk(sk, ntq, [&](long bi, int t0, int cnt, int seg) {
     const int kb = (int)(bi % nkb);
     const long nh = bi / nkb;
@@ -1920,7 +1971,8 @@ bool pp_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env
   const bool forced = env && atoi(env) == 2;
   const long units = (long)((t + PP_QPB - 1) / PP_QPB) * heads * nb;
   const int ntile = (t + 63) / 64;
-  const long G = device_cus();
+  const char* ge = getenv("DC_ATTN_PP_G");   // grid size override (experiments)
+  const long G = ge && atoi(ge) > 0 ? atoi(ge) : device_cus();
   const long U = units * ntile;
   if (!forced && U < 16 * G) return false;
   if (units > kAttnCounterBytes / 4) return false;
