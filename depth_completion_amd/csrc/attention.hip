@@ -1966,9 +1966,12 @@ bool launch_fwd_sk(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, i
 // stream-K plan of the 8-wave ping-pong kernels over (256-query block, key tile): one block per CU; NV fp32
 // partial values per lane and slab slot; false when it does not apply (env: "0" off, "2" wherever it fits)
 bool pp_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env_name, int nv, AttnSK& sk) {
+  // opt-in: measured no faster than the one-barrier-per-tile kernels (level 0 fwd 101 vs 104 us, bwd 275 vs 272 us;
+  // slower at levels 1-2, profiles/r04n): both are bound by the softmax's VALU issue, which the phase split does
+  // not shorten
   const char* env = getenv(env_name);   // read per launch (host side, once per captured graph node)
-  if (!ws || (env && atoi(env) == 0) || getenv("DC_ATTN_CFG")) return false;
-  const bool forced = env && atoi(env) == 2;
+  if (!ws || !env || atoi(env) == 0 || getenv("DC_ATTN_CFG")) return false;
+  const bool forced = atoi(env) == 2;
   const long units = (long)((t + PP_QPB - 1) / PP_QPB) * heads * nb;
   const int ntile = (t + 63) / 64;
   const char* ge = getenv("DC_ATTN_PP_G");   // grid size override (experiments)
@@ -1988,8 +1991,8 @@ bool pp_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env
 }
 
 // Ping-pong forward (attn_fwd_pp_kernel): one 8-wave block per CU, stream-K over (256-query block, key tile).
-// Default wherever every block gets >= 16 key tiles (UNet levels 0 and 1 at batch 1); DC_ATTN_PP=0 disables it,
-// 2 takes it wherever the slab fits (tests); a forced DC_ATTN_CFG bypasses it.
+// Opt-in: DC_ATTN_PP=1 wherever every block gets >= 16 key tiles, 2 wherever the slab fits (tests); a forced
+// DC_ATTN_CFG bypasses it.
 bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, float* ws,
                    long ws_bytes, hipStream_t st) {
   AttnSK sk;
@@ -1998,7 +2001,7 @@ bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, i
   return true;
 }
 
-// Ping-pong dQ (attn_bwd_dq_pp_kernel), same policy as the forward's; DC_ATTN_PP_DQ=0 disables it.
+// Ping-pong dQ (attn_bwd_dq_pp_kernel), same policy as the forward's (DC_ATTN_PP_DQ=1 / 2).
 bool launch_dq_pp(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
                   float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes,
                   hipStream_t st) {
@@ -2009,7 +2012,7 @@ bool launch_dq_pp(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* d
   return true;
 }
 
-// Ping-pong dK/dV (attn_bwd_dkdv_pp_kernel), same policy; DC_ATTN_PP_DKDV=0 disables it.
+// Ping-pong dK/dV (attn_bwd_dkdv_pp_kernel), same policy (DC_ATTN_PP_DKDV=1 / 2).
 bool launch_dkdv_pp(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
                     int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
   AttnSK sk;
