@@ -252,11 +252,15 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
         cands += [(a, s) for a in range(SKINNY_FIRST, RESIDENT_FIRST)
                   for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, -2, -4, -6, -8, -10, -12, -16, -20)
                   if abs(s) <= d.cin // 64 and SKINNY_TAPS[a - SKINNY_FIRST] == taps]
+    if halo_eligible(d) and d.cin == 64 and d.cout <= 64 and not d.gn and not d.x2:
+        cands += [(a, b) for a in range(RESIDENT_FIRST, WIDE_FIRST) for b in (0, 1, 2, 3)]
+    if d.gn:
+        # a GroupNorm-fused call runs skinny / resident / wide choices as the library heuristic (those kernels have
+        # no fused-statistics epilogue): never offer them, so the table only holds configurations that were timed
+        cands = [c for c in cands if not SKINNY_FIRST <= c[0] <= WIDE_LAST]
     if getattr(ctx, "tune_only", None):   # tools/tune_gemm.py --try: the committed choice against these algos only
         cur = ctx.tune_only[1].get(conv_key(d))
         cands = ([cur] if cur else []) + [c for c in cands if c[0] in ctx.tune_only[0]]
-    if halo_eligible(d) and d.cin == 64 and d.cout <= 64 and not d.gn and not d.x2:
-        cands += [(a, b) for a in range(RESIDENT_FIRST, WIDE_FIRST) for b in (0, 1, 2, 3)]
     best, best_t = (0, 0), float("inf")
     # DC_TUNE_COLD=1: every timed call starts with L2 and the Infinity Cache flushed (a 512 MiB write),
     # as the weights are in the sampler step (each is touched once per pass)
