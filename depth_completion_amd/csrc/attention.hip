@@ -342,12 +342,30 @@ __device__ __forceinline__ bool sk_handoff_fwd(const AttnSK& sk, char* smem, lon
   return true;
 }
 
+// max of three without the IEEE-mode canonicalisation fmaxf gets (one v_max_f32 x, x, x per operand): the
+// softmax inputs are MFMA results, NaN-free by construction
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// max over the two lanes of a row (lane l and l ^ 32) by v_permlane32_swap (no LDS round trip)
+__device__ __forceinline__ float rowmax_pair(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return max3_raw(__uint_as_float(r[0]), __uint_as_float(r[1]), x);
+}
+__device__ __forceinline__ float rowsum_pair(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ------------------------------------------------------------------------------ forward
 // KS key-splits per block: waves QW p .. QW p + QW - 1 sweep the p-th contiguous range of key tiles
 // for the same 32 QW queries, then the partial (m, l, O) are merged through LDS in a fixed order.
 // K / V tiles stream through an S-deep LDS-DMA ring per split (one barrier per tile).
 constexpr int FWD_S = 3;
 constexpr float FWD_TAU = 8.0f;  // lazy-rescale slack (natural-log units of the scaled scores)
+constexpr float FWD_SUM_TAU = 2980.9579870417283f;   // e^FWD_TAU: the row-sum form of the same bound
 template <int QW, int KS>
 struct FwdLds {
   static constexpr int STAGE = 2 * TILE_B;                      // K + V
@@ -356,7 +374,7 @@ struct FwdLds {
   static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
-template <int QW, int KS, bool SK>
+template <int QW, int KS, bool SK, bool FS>
 __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo,
                                             float* lse, int qbk, int h, int n, int t0, int tcount, const AttnSK& sk,
                                             long bi, int seg) {
@@ -442,38 +460,91 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
             if (key >= T) sacc[b][r] = -INFINITY;
           }
       }
-      float mx = -INFINITY;
+      if constexpr (!FS) {
+        float mx = -INFINITY;
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[b][r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      // lazy rescale: the reference max moves only when a row max exceeds it by more than FWD_TAU, so
-      // weights stay <= e^FWD_TAU (exact in fp32 / bf16 relative terms; O and l share the reference)
-      if (__any(mx > m + FWD_TAU)) {
-        const float mnew = fmaxf(m, mx);
-        const float alpha = fast_exp2((m - mnew) * LOG2E);
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[b][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        // lazy rescale: the reference max moves only when a row max exceeds it by more than FWD_TAU, so
+        // weights stay <= e^FWD_TAU (exact in fp32 / bf16 relative terms; O and l share the reference)
+        if (__any(mx > m + FWD_TAU)) {
+          const float mnew = fmaxf(m, mx);
+          const float alpha = fast_exp2((m - mnew) * LOG2E);
 #pragma unroll
-        for (int db = 0; db < 2; ++db)
+          for (int db = 0; db < 2; ++db)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-        l *= alpha;
-        m = mnew;
-      }
-      // row sums in fp32 from the unrounded weights: the LSE the backward recomputes P from must not carry
-      // P's bf16 rounding (a sum of bf16 P, e.g. on the MFMA pipe, is off by up to ~4e-3 in the LSE on
-      // peaked rows and biases the guidance gradient: tools/attn_acc.py, profiles/r02m)
-      const float ml = m * LOG2E;
-      float ps = 0.0f;
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
-          sacc[b][r] = pv;
-          ps += pv;
+            for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+          l *= alpha;
+          m = mnew;
         }
-      l += ps;
+        // row sums in fp32 from the unrounded weights: the LSE the backward recomputes P from must not carry
+        // P's bf16 rounding (a sum of bf16 P, e.g. on the MFMA pipe, is off by up to ~4e-3 in the LSE on
+        // peaked rows and biases the guidance gradient: tools/attn_acc.py, profiles/r02m)
+        const float ml = m * LOG2E;
+        float ps = 0.0f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+            sacc[b][r] = pv;
+            ps += pv;
+          }
+        l += ps;
+      } else {
+        // (DC_ATTN_FASTSM) the same lazy rescale decided from the row sum: exponentiate against the current
+        // reference max first; a row sum <= e^FWD_TAU bounds every weight of the row by it, so the 32-value max
+        // is needed only when some row's sum exceeds that (rare; always on the first tile, where m = -inf)
+        float p[2][16];
+        float ml = m * LOG2E;
+        float ps0 = 0.0f, ps1 = 0.0f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            p[b][r] = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+            if (r & 1) ps1 += p[b][r];
+            else ps0 += p[b][r];
+          }
+        float ps = rowsum_pair(ps0 + ps1);
+        if (__any(!(ps <= FWD_SUM_TAU))) {
+          float mx0 = max3_raw(sacc[0][0], sacc[0][1], sacc[0][2]);
+          float mx1 = max3_raw(sacc[1][0], sacc[1][1], sacc[1][2]);
+#pragma unroll
+          for (int r = 3; r < 15; r += 2) {
+            mx0 = max3_raw(mx0, sacc[0][r], sacc[0][r + 1]);
+            mx1 = max3_raw(mx1, sacc[1][r], sacc[1][r + 1]);
+          }
+          const float mx = rowmax_pair(max3_raw(max3_raw(mx0, mx1, sacc[0][15]), sacc[1][15], sacc[1][15]));
+          const float mnew = fmaxf(m, mx);
+          const float alpha = fast_exp2((m - mnew) * LOG2E);
+#pragma unroll
+          for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+          l *= alpha;
+          m = mnew;
+          ml = m * LOG2E;
+          ps0 = ps1 = 0.0f;
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              p[b][r] = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+              if (r & 1) ps1 += p[b][r];
+              else ps0 += p[b][r];
+            }
+          ps = rowsum_pair(ps0 + ps1);
+        }
+        // (l holds the full row's sum here: both lane halves add the same value)
+        l += ps;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sacc[b][r] = p[b][r];
+      }
       // V^T fragments: two k-slices in flight ahead of the MFMAs that consume them
       constexpr int VIMM = ST * FwdLds<QW, KS>::STAGE + TILE_B;
       bf16x8 vf[4][2];
@@ -507,7 +578,7 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
   }
   vm_wait_n<0>();
   __syncthreads();
-  l += __shfl_xor(l, 32, 64);  // the two lane halves of a row hold the sums of alternate key groups
+  if constexpr (!FS) l += __shfl_xor(l, 32, 64);  // the two lane halves of a row hold alternate key groups' sums
   if constexpr (KS > 1) {
     // merge the key-split partials: parts 1.. publish (m, l, O) per lane, part 0 folds them in order
     float* red = reinterpret_cast<float*>(smem);
@@ -573,20 +644,20 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
 }
 
 
-template <int QW, int KS, bool SK>
+template <int QW, int KS, bool SK, bool FS>
 __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(
     const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse, AttnSK sk) {
   __shared__ __attribute__((aligned(16))) char smem[FwdLds<QW, KS>::BYTES];
   const int ntk = (T + 63) / 64;
   if constexpr (!SK) {
-    fwd_segment<QW, KS, false>(smem, qkv, ld, T, heads, o, ldo, lse, blockIdx.x, blockIdx.y, blockIdx.z, 0, ntk, sk,
+    fwd_segment<QW, KS, false, FS>(smem, qkv, ld, T, heads, o, ldo, lse, blockIdx.x, blockIdx.y, blockIdx.z, 0, ntk, sk,
                                0, 0);
   } else {
     const int nqb = (T + 32 * QW - 1) / (32 * QW);
     sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
       const int qbk = (int)(bi % nqb);
       const long nh = bi / nqb;
-      fwd_segment<QW, KS, true>(smem, qkv, ld, T, heads, o, ldo, lse, qbk, (int)(nh % heads), (int)(nh / heads), t0,
+      fwd_segment<QW, KS, true, FS>(smem, qkv, ld, T, heads, o, ldo, lse, qbk, (int)(nh % heads), (int)(nh / heads), t0,
                                 cnt, sk, bi, seg);
     });
   }
@@ -612,23 +683,6 @@ __device__ __forceinline__ bf16x8 ds_read128_nw(unsigned addr) {
   bf16x8 r;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(IMM));
   return r;
-}
-
-// max of three without the IEEE-mode canonicalisation fmaxf gets (one v_max_f32 x, x, x per operand): the
-// softmax inputs are MFMA results, NaN-free by construction
-__device__ __forceinline__ float max3_raw(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-// max over the two lanes of a row (lane l and l ^ 32) by v_permlane32_swap (no LDS round trip)
-__device__ __forceinline__ float rowmax_pair(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return max3_raw(__uint_as_float(r[0]), __uint_as_float(r[1]), x);
-}
-__device__ __forceinline__ float rowsum_pair(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 // ring stage PP_S - 1 zeroed once per block before its first walk segment: the t = 0 MFMA phase multiplies that
@@ -1840,6 +1894,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void a
 }  // namespace
 
 namespace {
+// forward softmax with the lazy rescale decided from the row sum (fwd_segment FS); DC_ATTN_FASTSM=0 / 1
+bool fast_softmax() {
+  const char* e = getenv("DC_ATTN_FASTSM");   // read per launch (host side, once per captured graph node)
+  return e && atoi(e) != 0;
+}
+
 // (query waves per block, key splits per block): chosen per launch by a makespan model over the
 // 256 CUs -- rounds of blocks x per-block work (QW) -- discounted when fewer than 8 waves are
 // resident per CU.  DC_ATTN_CFG=<index> forces one (tests / benchmarks).
@@ -1877,8 +1937,12 @@ template <int QW, int KS>
 void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
   const AttnSK none{};
-  hipLaunchKernelGGL((attn_fwd_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o, ldo, lse,
-                     none);
+  if (fast_softmax())
+    hipLaunchKernelGGL((attn_fwd_kernel<QW, KS, false, true>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o,
+                       ldo, lse, none);
+  else
+    hipLaunchKernelGGL((attn_fwd_kernel<QW, KS, false, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o,
+                       ldo, lse, none);
 }
 
 // dQ first: it computes delta = rowsum(dO * O) for its resident queries and publishes it; dK/dV (next
@@ -1958,8 +2022,8 @@ bool launch_fwd_sk(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, i
   const char* on = getenv("DC_ATTN_SK_FWD");
   if (!on || atoi(on) == 0 || (getenv("DC_ATTN_SK") && atoi(getenv("DC_ATTN_SK")) == 0)) return false;
   if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK_FWD", sk)) return false;
-  hipLaunchKernelGGL((attn_fwd_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, t, heads, o, ldo,
-                     lse, sk);
+  hipLaunchKernelGGL((attn_fwd_kernel<4, 1, true, false>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, t, heads, o,
+                     ldo, lse, sk);
   return true;
 }
 

@@ -505,6 +505,36 @@ def test_attention_fwd_stream_k(ctx, n, t, heads, monkeypatch):
     assert rel(outs["2"][1], lse_ref) < 1e-4
 
 
+@pytest.mark.parametrize("n,t,heads,peak", [(1, 64, 1, 1.0), (1, 65, 2, 1.0), (2, 300, 2, 1.0), (1, 1000, 5, 1.0),
+                                            (1, 1000, 5, 6.0), (1, 6912, 5, 1.0), (1, 6912, 5, 4.0)])
+def test_attention_fwd_fastsm(ctx, n, t, heads, peak, monkeypatch):
+    """Forward softmax with the lazy rescale decided from the row sum (DC_ATTN_FASTSM=1): bit-identical on repeat,
+    equal to the max-decided form up to the reference-max choice, and against fp32 SDPA / logsumexp.  `peak` scales
+    the queries so that scores are peaked (rows whose sum crosses e^8 mid-sweep, the recompute path)."""
+    from depth_completion_amd import ops
+    C = heads * 64
+    qkv = rnd(n, t, 3 * C, seed=41).to(torch.bfloat16).float()
+    qkv[..., :C] *= peak
+    qkv = qkv.to(torch.bfloat16).float()
+    q, k, v = qkv.split(C, -1)
+    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
+    ref = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
+    lse_ref = torch.logsumexp(torch.einsum("nhqd,nhkd->nhqk", sh(q), sh(k)) / 8, -1)
+    qkv_b = qkv.to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
+    outs = {}
+    for mode in ("0", "1", "1b"):
+        monkeypatch.setenv("DC_ATTN_FASTSM", mode[0])
+        ob = torch.zeros(n * t, C, dtype=torch.bfloat16, device=dev)
+        lse = torch.zeros(n, heads, t, device=dev)
+        ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
+        torch.cuda.synchronize()
+        outs[mode] = (ob, lse)
+    assert torch.equal(outs["1"][0], outs["1b"][0]) and torch.equal(outs["1"][1], outs["1b"][1])
+    assert rel(outs["1"][0], outs["0"][0]) < 5e-3
+    assert rel(outs["1"][0].view(n, t, C), ref) < 1e-2
+    assert rel(outs["1"][1], lse_ref) < 1e-4
+
+
 @pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (1, 65, 2), (1, 300, 2), (3, 257, 2), (2, 1000, 3), (1, 1728, 10),
                                        (1, 6912, 5)])
 def test_attention_fwd_pingpong(ctx, n, t, heads, monkeypatch):

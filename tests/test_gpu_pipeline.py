@@ -272,7 +272,10 @@ def test_nearest_interp(kw):
     lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
     lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
     print(f"\nnearest {kw}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
-    assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
+    # the oracle's own bf16 |d| error is one sample of a spread (train_latents=False: 0.006 - 0.027 across GPU runs,
+    # profiles/r03_suite, r03v, r03z, r04za -- torch's bf16 GPU path is not run-to-run deterministic), so the depth
+    # bound takes it no lower than 0.01; the latent bound stays relative
+    assert err_h <= 2 * max(err_b, 0.01) + 2e-3 and lat_h <= 2 * lat_b + 2e-3
     # blocky: every output pixel equals one decoded pixel, so the dense map has at most PH*PW levels per frame
     assert dh.unique().numel() <= 48 * 64
 

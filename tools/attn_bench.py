@@ -15,6 +15,7 @@ from depth_completion_amd.ops import Ctx  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--no-bwd", action="store_true")
+ap.add_argument("--env", default="DC_ATTN_PP", help="forward A/B switch (0 vs 2): DC_ATTN_PP or DC_ATTN_FASTSM")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 ctx = Ctx(dev)
@@ -45,9 +46,9 @@ for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (8, 6912, 5), (8,
     res = {"0": [], "2": []}
     for _ in range(args.reps):
         for mode in ("0", "2"):
-            os.environ["DC_ATTN_PP"] = mode
+            os.environ[args.env] = mode
             res[mode].append(timed(lambda: ops.attn_fwd(ctx, qkv, n, t, heads, o, lse)))
-    for mode, name in (("0", "fwd"), ("2", "fwd-pp")):
+    for mode, name in (("0", "fwd"), ("2", f"fwd-{args.env}")):
         ms = min(res[mode])
         print(f"n={n} T={t} H={heads} {name}: {ms*1e3:.1f} us  {f/ms/1e9:.0f} TF/s  (all: "
               f"{' '.join(f'{x*1e3:.1f}' for x in res[mode])})", flush=True)
