@@ -1,11 +1,11 @@
 #!/bin/bash
-# A/B of environment settings on the C2 bench line, alternating on one box (2 rounds):
+# A/B of environment settings on the C2 bench line, alternating on one box (REPS rounds, default 2):
 #   bash tools/ab/env_ab.sh <tag> "" "DC_GN_GROUP=0" ...      ("" = the defaults)
 set -e
 tag=${1:?tag}; shift
 out=gpurun_out/$tag
 mkdir -p "$out"
-for rep in 1 2; do
+for rep in $(seq 1 "${REPS:-2}"); do
   i=0
   for e in "$@"; do
     i=$((i + 1))
