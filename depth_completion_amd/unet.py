@@ -192,6 +192,7 @@ class UNetPlan:
         n_gn = 2 * (2 * n_res + n_tr + 1)
         self._gn_words = ops.gn_acc_words(nb, self.groups)
         self.gn_arena = torch.zeros(n_gn * self._gn_words, dtype=torch.int64, device=dev)
+        self._gn_slots = n_gn
         self._gn_next = 0
         self._gn_targets: dict = {}   # id(tensor) -> [(acc, coff, groups, cpg, hw)]
         self._gn_fuse: dict = {}      # id(tensor) -> ops.GnFuse, built at the first call
@@ -213,6 +214,8 @@ class UNetPlan:
     # ------------------------------------------------------------------ fused GroupNorm statistics
     def _gn_acc(self) -> torch.Tensor:
         i = self._gn_next
+        if i >= self._gn_slots:   # a GroupNorm site the arena was not sized for: fail, never hand out past the end
+            raise RuntimeError(f"GroupNorm accumulator arena exhausted ({self._gn_slots} slots)")
         self._gn_next += 1
         return self.gn_arena[i * self._gn_words:(i + 1) * self._gn_words]
 
