@@ -192,9 +192,22 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
     from oracle import pipeline_ref as P
     from oracle.diffusers_ref import (AutoencoderTiny, DDIMScheduler, UNet2DConditionModel, synthetic_state_dict,
                                       synthetic_taesd_state_dict, synthetic_text_embedding)
-    # every CPU this process may run on (the reference's CPU path on the host's cores)
-    threads = len(os.sched_getaffinity(0))
+    # the CPUs this process may run on (the reference's CPU path on the host's cores): the
+    # affinity mask, capped by OMP_NUM_THREADS where the host declares its CPU share that way (the GPU boxes show
+    # every CPU of the machine in the mask but give a job 16; more threads than that oversubscribe the share)
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
     torch.set_num_threads(threads)
+    # heartbeat on stderr while the oracle runs (a silent minute-long CPU leg must not look hung)
+    import threading
+    done = threading.Event()
+
+    def beat():
+        t0 = time.perf_counter()
+        while not done.wait(30.0):
+            log(f"cpu baseline: running ({time.perf_counter() - t0:.0f} s)")
+    threading.Thread(target=beat, daemon=True).start()
     unet = UNet2DConditionModel()
     unet.load_state_dict(synthetic_state_dict(unet, 11))
     vae = AutoencoderTiny()
@@ -208,11 +221,13 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
         pipe(img[None], sp[None], 120.0, norm="const", steps=s, resolution=768)
         times[s] = time.perf_counter() - t0
         log(f"cpu baseline: {s}-step oracle call {times[s]:.1f} s on {threads} threads")
+    done.set()
     t_step = max(times[2] - times[1], 1e-3)
     t_fixed = max(times[1] - t_step, 0.0)
     t_frame = (t_fixed + steps * t_step) * seeds
     return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads,
-            "cores_label": f"{threads} threads = CPUs in this process's affinity mask ({os.cpu_count()} host CPUs)",
+            "cores_label": f"{threads} threads: affinity mask {aff} CPUs, OMP_NUM_THREADS {omp or 'unset'}, "
+                           f"{os.cpu_count()} host CPUs",
             "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"oracle bf16 CPU pipeline, 1 frame {w}x{h}, 1- and 2-step calls "
