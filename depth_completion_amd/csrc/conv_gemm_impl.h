@@ -215,6 +215,11 @@ __device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, 
 // loaded at kernel start (or before the staging barrier where the registers are scarce) they land under the main
 // loop.  RMAX = the lane's 16-B output rows (lane + 64 r of the wave's WM x WN / 8 row-vectors; GPR divides 64, so a
 // lane keeps one 8-channel column group).
+// kEpiEarly: load them at kernel start.  Off: holding them across the main loop cost 20-90 VGPRs in most im2col
+// instantiations (128 x 128 x 32: 140 -> 228, 128 x 64 x 64: 144 -> 188) and a wave per SIMD of occupancy, which the
+// runtime A/B (DC_HALO_DIAG=256, same binary) could not show: C3 conv launches +21 % (profiles/r04z).  The epilogue
+// then loads every operand after the main loop (the round-3 placement).
+constexpr bool kEpiEarly = false;
 template <int NJ, int RMAX>
 struct EpiPre {
   float cv[NJ];        // per-column bias (GNM 3: csum)
@@ -881,8 +886,8 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
   const int wm = wid >> 1, wn = wid & 1;
   const long M = conv_rows(p);
   const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-  if (!TileEpi<BM, BN>::kEarly || (p.diag & 256)) tile_epi_load<BM, BN, GNM>(p, m0, n0, true, pre);
-  if (p.diag & 256) tile_epi_load<BM, BN, GNM>(p, m0, n0, false, pre);   // A/B: the late (round-3) placement
+  if (kEpiEarly && (!TileEpi<BM, BN>::kEarly || (p.diag & 256))) tile_epi_load<BM, BN, GNM>(p, m0, n0, true, pre);
+  if (!kEpiEarly || (p.diag & 256)) tile_epi_load<BM, BN, GNM>(p, m0, n0, false, pre);   // the late placement
   __syncthreads();  // every wave is done reading the ring
   constexpr int LDE = WN + 8;
   bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
@@ -979,7 +984,7 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
     return;
   }
   if (p.diag & 64) return;   // experiments only: no epilogue stores
-  if constexpr (!TileEpi<BM, BN>::kRows) {
+  if constexpr (!TileEpi<BM, BN>::kRows || !kEpiEarly) {   // each row's operands loaded as it is stored
 #pragma unroll 4
     for (int g = lane; g < WM * GPR; g += 64) {
       const int row = g / GPR, cg = g - (g / GPR) * GPR;
@@ -1050,7 +1055,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     const int kc_begin = split * p.kps;
     const int kc_end = min(nk, kc_begin + p.kps);
     // the epilogue's column operands (and, where registers allow, its row operands) in flight under the main loop
-    if (!(p.diag & 256)) {
+    if (kEpiEarly && !(p.diag & 256)) {
       tile_epi_load<BM, BN, GNM>(p, m0, n0, false, pre);
       if (TileEpi<BM, BN>::kEarly) tile_epi_load<BM, BN, GNM>(p, m0, n0, true, pre);
     }
@@ -1080,7 +1085,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvGemmParams p) 
     tile_coords(p, tile, p.splits / tiles_n, tiles_n, tm, tn);
     const long m0 = (long)tm * BM;
     const int n0 = tn * BN;
-    if (!(p.diag & 256)) {
+    if (kEpiEarly && !(p.diag & 256)) {
       tile_epi_load<BM, BN, GNM>(p, m0, n0, false, pre);
       if (TileEpi<BM, BN>::kEarly) tile_epi_load<BM, BN, GNM>(p, m0, n0, true, pre);
     }
@@ -1349,7 +1354,7 @@ struct HaloBlock {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the epilogue's column (and, where registers allow, row) operands in flight under the main loop
-    if (!(p.diag & 256)) {
+    if (kEpiEarly && !(p.diag & 256)) {
       epi_cols<0>(p, n0 + wn * WN + (lane & 15), pre);
       if (kEarly) epi_load_rows();
     }
@@ -1383,8 +1388,8 @@ struct HaloBlock {
   __device__ __forceinline__ void epilogue() {
     const int wid = threadIdx.x >> 6;
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;
-    if (!kEarly || (p.diag & 256)) epi_load_rows();
-    if (p.diag & 256) epi_cols<0>(p, n0 + wn * WN + (lane & 15), pre);   // A/B: the late (round-3) placement
+    if (kEpiEarly && (!kEarly || (p.diag & 256))) epi_load_rows();
+    if (!kEpiEarly || (p.diag & 256)) epi_cols<0>(p, n0 + wn * WN + (lane & 15), pre);   // the late placement
     __syncthreads();
     constexpr int LDE = WN + 8;
     bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
@@ -1415,6 +1420,17 @@ struct HaloBlock {
     }
     if (p.diag & 64) return;   // experiments only: no epilogue stores
     const int cg = lane % GPR, c = n0 + wn * WN + cg * 8;
+    if constexpr (!kEpiEarly) {   // each row's operands loaded as it is stored
+#pragma unroll 4
+      for (int g = lane; g < WM * GPR; g += 64) {
+        const long m = out_pix(g / GPR);
+        if (m < 0 || c >= p.cout) continue;
+        float v[8];
+        load8(es + (g / GPR) * LDE + cg * 8, v);
+        epilogue_store(p, m, c, v, false);
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) {
       if (pre.mrow[r] < 0) continue;
