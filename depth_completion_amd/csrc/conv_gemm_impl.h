@@ -893,25 +893,25 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
   bf16* es = reinterpret_cast<bf16*>(smem) + wid * WM * LDE;
   DC_LDS_ASSERT((wid * WM * LDE) * 2, WM * LDE * 2, (Cfg<BM, BN, 64, 2>::EPI));
   if constexpr (GNM == 3) {
-    // LayerNorm folded in: y = rstd (acc - mean csum[c]) + cbias[c], the rows' (mean, rstd) from p.ln_stats
-    float mu[MI][4], rs[MI][4];
+    // LayerNorm folded in: y = rstd (acc - mean csum[c]) + cbias[c], the rows' (mean, rstd) from p.ln_stats, one
+    // 16-row slice at a time (all MI slices' statistics at once cost the 128 x 128 tiles a wave per SIMD)
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i) {
+      float mu[4], rs[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const long m = m0 + wm * WM + i * 16 + row_l + e;
         const bool in = m < M;
-        mu[i][e] = in ? p.ln_stats[m * 2] : 0.0f;
-        rs[i][e] = in ? p.ln_stats[m * 2 + 1] : 0.0f;
+        mu[e] = in ? p.ln_stats[m * 2] : 0.0f;
+        rs[e] = in ? p.ln_stats[m * 2 + 1] : 0.0f;
       }
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const float cs = pre.cv[j], cb = pre.cv2[j];
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int j = 0; j < NJ; ++j) {
+        const float cs = pre.cv[j], cb = pre.cv2[j];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          es[(i * 16 + row_l + e) * LDE + j * 16 + col_l] = (bf16)(rs[i][e] * (acc[i][j][e] - mu[i][e] * cs) + cb);
+          es[(i * 16 + row_l + e) * LDE + j * 16 + col_l] = (bf16)(rs[e] * (acc[i][j][e] - mu[e] * cs) + cb);
+      }
     }
   } else {
 #pragma unroll
