@@ -18,7 +18,17 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def record(out, batch):
+    import threading
+    import time
     import torch
+    # heartbeat: under rocprofv3 --pmc every dispatch is serialised and a pass runs minutes without other output
+    t_start = time.perf_counter()
+
+    def beat():
+        while True:
+            time.sleep(30.0)
+            print(f"step_profile: running ({time.perf_counter() - t_start:.0f} s)", flush=True)
+    threading.Thread(target=beat, daemon=True).start()
     from bench import conv_flops, synth_frame
     from depth_completion_amd import ops, synthetic
     from depth_completion_amd._lib import ConvDesc
