@@ -185,6 +185,26 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cgroup_cpu_quota():
+    """The CPU quota of this process's cgroup as (label, CPUs): cgroup v2 cpu.max ("max 100000" = unlimited, or
+    "<quota> <period>" microseconds), else cgroup v1 cfs_quota / cfs_period; CPUs None when unlimited or unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q == "max":
+            return f"cpu.max {q} {per} (unlimited)", None
+        return f"cpu.max {q} {per}", int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q <= 0:
+            return f"cfs_quota_us {q} (unlimited)", None
+        return f"cfs_quota_us {q} / cfs_period_us {per}", q / per
+    except (OSError, ValueError):
+        return "no cgroup CPU quota readable", None
+
+
 def cpu_baseline(h, w, n_points, steps, seeds, pattern):
     """Oracle (CPU restatement) timed on this host: 1- and 2-step calls of one seed, extrapolated to the
     run's guided steps and seeds (an ensemble frame = `seeds` independent samples + a negligible fit)."""
@@ -198,6 +218,9 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
     aff = len(os.sched_getaffinity(0))
     omp = os.environ.get("OMP_NUM_THREADS", "")
     threads = min(aff, int(omp)) if omp.isdigit() and int(omp) > 0 else aff
+    quota_label, quota = cgroup_cpu_quota()
+    if quota is not None:   # never more threads than the cgroup's CPU quota grants
+        threads = max(1, min(threads, int(quota)))
     torch.set_num_threads(threads)
     # heartbeat on stderr while the oracle runs (a silent minute-long CPU leg must not look hung)
     import threading
@@ -227,7 +250,8 @@ def cpu_baseline(h, w, n_points, steps, seeds, pattern):
     t_frame = (t_fixed + steps * t_step) * seeds
     return {"value": 1.0 / t_frame, "unit": "frames/s", "cores": threads,
             "cores_label": f"{threads} threads: affinity mask {aff} CPUs, OMP_NUM_THREADS {omp or 'unset'}, "
-                           f"{os.cpu_count()} host CPUs",
+                           f"cgroup {quota_label}, {os.cpu_count()} host CPUs",
+            "cgroup_cpu_quota": quota,
             "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"oracle bf16 CPU pipeline, 1 frame {w}x{h}, 1- and 2-step calls "

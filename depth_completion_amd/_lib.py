@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -73,7 +73,6 @@ _SIGS = {
                          vp, i32, vp, vp],
     "dc_gn_acc_bytes": [i32, i32],
     "dc_gn_fuse_pays": [i32, i32, i32, i32],
-    "dc_gn_coop_timeouts": [],
     "dc_groupnorm_fwd_acc": [vp, i32, vp, i32, i32, i32, i32, i32, i32, f32, vp, vp, i32, vp, vp, i32, vp, vp],
     "dc_groupnorm_bwd_acc": [vp, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, vp, i32, vp, i32,
                              vp, i32, vp],
@@ -119,6 +118,7 @@ _SIGS = {
     "dc_mask_rows_ws_bytes": [i64],
     "dc_mask_count": [vp, i64, vp, vp, vp],
     "dc_mask_rows": [vp, i64, vp, vp, i32, vp, vp],
+    "dc_pad_rows": [vp, vp, i32, vp],
     "dc_memset_async": [vp, i32, i64, vp],
     "dc_latent_scale_fwd": [vp, i32, i64, f32, vp, vp],
     "dc_latent_scale_bwd": [vp, i32, i64, f32, vp, vp, vp, vp, vp],

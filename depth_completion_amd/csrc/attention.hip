@@ -305,43 +305,6 @@ __device__ __forceinline__ void sk_walk(const AttnSK& sk, int ntile, F&& seg_fn)
   }
 }
 
-// forward hand-off: partial (m, l, O) per lane; the last arriver folds every covering block's partial in
-// block order with the online-softmax rescale (m = max, l and O scaled by exp(m_i - m))
-template <int QW>
-__device__ __forceinline__ bool sk_handoff_fwd(const AttnSK& sk, char* smem, long bi, int ntile, int seg,
-                                               float (&v)[34]) {
-  float t[34];
-#pragma unroll
-  for (int e = 0; e < 34; ++e) t[e] = v[e];
-  // publish, count, and (last arriver) gather the raw partials; the fold below replaces the plain sum
-  if (!sk_handoff<QW, 34, false>(sk, smem, bi, ntile, seg, t)) return false;
-  // sk_handoff<..., false> leaves the partials of the covering blocks unsummed: re-read them in order
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const long x0 = bi * ntile, x1 = x0 + ntile - 1;
-  const long bf = sk_block_of(sk, x0), bl = sk_block_of(sk, x1);
-  bool first = true;
-  for (long bb = bf; bb <= bl; ++bb) {
-    const long sg = bi - sk_start(sk, bb) / ntile;
-    const float* src = sk.slab + (((bb * sk.spb + sg) * QW + wid) * 34) * 64 + lane;
-    float p[34];
-#pragma unroll
-    for (int e = 0; e < 34; ++e) p[e] = __hip_atomic_load(src + e * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (first) {
-#pragma unroll
-      for (int e = 0; e < 34; ++e) v[e] = p[e];
-      first = false;
-      continue;
-    }
-    const float mn = fmaxf(v[0], p[0]);
-    const float a0 = fast_exp2((v[0] - mn) * LOG2E), a1 = fast_exp2((p[0] - mn) * LOG2E);
-    v[1] = v[1] * a0 + p[1] * a1;
-#pragma unroll
-    for (int e = 2; e < 34; ++e) v[e] = v[e] * a0 + p[e] * a1;
-    v[0] = mn;
-  }
-  return true;
-}
-
 // max of three without the IEEE-mode canonicalisation fmaxf gets (one v_max_f32 x, x, x per operand): the
 // softmax inputs are MFMA results, NaN-free by construction
 __device__ __forceinline__ float max3_raw(float a, float b, float c) {
@@ -374,10 +337,9 @@ struct FwdLds {
   static constexpr int BYTES = RING > RED ? RING : RED;
 };
 
-template <int QW, int KS, bool SK, bool FS>
+template <int QW, int KS>
 __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo,
-                                            float* lse, int qbk, int h, int n, int t0, int tcount, const AttnSK& sk,
-                                            long bi, int seg) {
+                                            float* lse, int qbk, int h, int n, int t0, int tcount) {
   constexpr int NT = 64 * QW;
   constexpr int S = FWD_S;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
@@ -460,91 +422,45 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
             if (key >= T) sacc[b][r] = -INFINITY;
           }
       }
-      if constexpr (!FS) {
-        float mx = -INFINITY;
+      // row max: four independent v_max3 chains over the lane's 32 scores (raw v_max3: no canonicalising fmaxf on
+      // the MFMA results, and no 32-deep serial chain), then the row's other lane half by v_permlane32_swap
+      float mc[4];
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[b][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        // lazy rescale: the reference max moves only when a row max exceeds it by more than FWD_TAU, so
-        // weights stay <= e^FWD_TAU (exact in fp32 / bf16 relative terms; O and l share the reference)
-        if (__any(mx > m + FWD_TAU)) {
-          const float mnew = fmaxf(m, mx);
-          const float alpha = fast_exp2((m - mnew) * LOG2E);
-#pragma unroll
-          for (int db = 0; db < 2; ++db)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-          l *= alpha;
-          m = mnew;
-        }
-        // row sums in fp32 from the unrounded weights: the LSE the backward recomputes P from must not carry
-        // P's bf16 rounding (a sum of bf16 P, e.g. on the MFMA pipe, is off by up to ~4e-3 in the LSE on
-        // peaked rows and biases the guidance gradient: tools/attn_acc.py, profiles/r02m)
-        const float ml = m * LOG2E;
-        float ps = 0.0f;
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
-            sacc[b][r] = pv;
-            ps += pv;
-          }
-        l += ps;
-      } else {
-        // (DC_ATTN_FASTSM) the same lazy rescale decided from the row sum: exponentiate against the current
-        // reference max first; a row sum <= e^FWD_TAU bounds every weight of the row by it, so the 32-value max
-        // is needed only when some row's sum exceeds that (rare; always on the first tile, where m = -inf)
-        float p[2][16];
-        float ml = m * LOG2E;
-        float ps0 = 0.0f, ps1 = 0.0f;
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            p[b][r] = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
-            if (r & 1) ps1 += p[b][r];
-            else ps0 += p[b][r];
-          }
-        float ps = rowsum_pair(ps0 + ps1);
-        if (__any(!(ps <= FWD_SUM_TAU))) {
-          float mx0 = max3_raw(sacc[0][0], sacc[0][1], sacc[0][2]);
-          float mx1 = max3_raw(sacc[1][0], sacc[1][1], sacc[1][2]);
-#pragma unroll
-          for (int r = 3; r < 15; r += 2) {
-            mx0 = max3_raw(mx0, sacc[0][r], sacc[0][r + 1]);
-            mx1 = max3_raw(mx1, sacc[1][r], sacc[1][r + 1]);
-          }
-          const float mx = rowmax_pair(max3_raw(max3_raw(mx0, mx1, sacc[0][15]), sacc[1][15], sacc[1][15]));
-          const float mnew = fmaxf(m, mx);
-          const float alpha = fast_exp2((m - mnew) * LOG2E);
-#pragma unroll
-          for (int db = 0; db < 2; ++db)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-          l *= alpha;
-          m = mnew;
-          ml = m * LOG2E;
-          ps0 = ps1 = 0.0f;
-#pragma unroll
-          for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              p[b][r] = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
-              if (r & 1) ps1 += p[b][r];
-              else ps0 += p[b][r];
-            }
-          ps = rowsum_pair(ps0 + ps1);
-        }
-        // (l holds the full row's sum here: both lane halves add the same value)
-        l += ps;
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) sacc[b][r] = p[b][r];
+      for (int c = 0; c < 4; ++c) {
+        const int b = c >> 1, r0 = 8 * (c & 1);
+        float t = max3_raw(sacc[b][r0], sacc[b][r0 + 1], sacc[b][r0 + 2]);
+        t = max3_raw(t, sacc[b][r0 + 3], sacc[b][r0 + 4]);
+        t = max3_raw(t, sacc[b][r0 + 5], sacc[b][r0 + 6]);
+        mc[c] = max3_raw(t, sacc[b][r0 + 7], sacc[b][r0 + 7]);
       }
+      const float mx = rowmax_pair(max3_raw(max3_raw(mc[0], mc[1], mc[2]), mc[3], mc[3]));
+      // lazy rescale: the reference max moves only when a row max exceeds it by more than FWD_TAU, so
+      // weights stay <= e^FWD_TAU (exact in fp32 / bf16 relative terms; O and l share the reference)
+      if (__any(mx > m + FWD_TAU)) {
+        const float mnew = fmaxf(m, mx);
+        const float alpha = fast_exp2((m - mnew) * LOG2E);
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+        l *= alpha;
+        m = mnew;
+      }
+      // row sums in fp32 from the unrounded weights: the LSE the backward recomputes P from must not carry
+      // P's bf16 rounding (a sum of bf16 P, e.g. on the MFMA pipe, is off by up to ~4e-3 in the LSE on
+      // peaked rows and biases the guidance gradient: tools/attn_acc.py, profiles/r02m)
+      // (four partial sums: independent add chains, summed in a fixed order)
+      const float ml = m * LOG2E;
+      float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+          sacc[b][r] = pv;
+          ps[r & 3] += pv;
+        }
+      l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
       // V^T fragments: two k-slices in flight ahead of the MFMAs that consume them
       constexpr int VIMM = ST * FwdLds<QW, KS>::STAGE + TILE_B;
       bf16x8 vf[4][2];
@@ -578,7 +494,7 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
   }
   vm_wait_n<0>();
   __syncthreads();
-  if constexpr (!FS) l += __shfl_xor(l, 32, 64);  // the two lane halves of a row hold alternate key groups' sums
+  l += __shfl_xor(l, 32, 64);  // the two lane halves of a row hold alternate key groups' sums
   if constexpr (KS > 1) {
     // merge the key-split partials: parts 1.. publish (m, l, O) per lane, part 0 folds them in order
     float* red = reinterpret_cast<float*>(smem);
@@ -607,25 +523,6 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
       m = mn;
     }
   }
-  if constexpr (SK) {
-    const int ntk = (T + 63) / 64;
-    if (!(t0 == 0 && tcount == ntk)) {   // query block shared with other blocks: merge (m, l, O) in block order
-      float v[34];
-      v[0] = m;
-      v[1] = l;
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[2 + 16 * db + r] = oacc[db][r];
-      if (!sk_handoff_fwd<QW>(sk, smem, bi, ntk, seg, v)) return;
-      m = v[0];
-      l = v[1];
-#pragma unroll
-      for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oacc[db][r] = v[2 + 16 * db + r];
-    }
-  }
   const float lsum = l;
   const float inv = 1.0f / lsum;
   if (qok) {
@@ -644,363 +541,11 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
 }
 
 
-template <int QW, int KS, bool SK, bool FS>
+template <int QW, int KS>
 __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_kernel(
-    const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse, AttnSK sk) {
+    const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse) {
   __shared__ __attribute__((aligned(16))) char smem[FwdLds<QW, KS>::BYTES];
-  const int ntk = (T + 63) / 64;
-  if constexpr (!SK) {
-    fwd_segment<QW, KS, false, FS>(smem, qkv, ld, T, heads, o, ldo, lse, blockIdx.x, blockIdx.y, blockIdx.z, 0, ntk, sk,
-                               0, 0);
-  } else {
-    const int nqb = (T + 32 * QW - 1) / (32 * QW);
-    sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
-      const int qbk = (int)(bi % nqb);
-      const long nh = bi / nqb;
-      fwd_segment<QW, KS, true, FS>(smem, qkv, ld, T, heads, o, ldo, lse, qbk, (int)(nh % heads), (int)(nh / heads), t0,
-                                cnt, sk, bi, seg);
-    });
-  }
-}
-
-// ------------------------------------------------------------------------ forward, ping-pong
-// Two waves per SIMD in opposite phases (MI355X_MICROARCH.md "Two waves per SIMD"): 8-wave blocks, one per
-// CU, each wave holding 32 queries of a 256-query block; all 8 waves share one K / V LDS-DMA ring.  The
-// waves 0-3 (half A) and 4-7 (half B, on the same four SIMDs) run the same per-tile program one segment
-// apart, block barriers between segments, so in every segment one wave of each SIMD is in its MFMA phase
-// (S^T of tile t = K Q^T, and O^T += V^T P^T of tile t - 1: 16 MFMAs, LDS fragments read by asm with counted
-// lgkm waits) while its partner runs the softmax of its own tile on the VALU (max, lazy rescale, exp2, row
-// sum, bf16 pack) -- the phases that the one-barrier-per-tile kernel above runs in lockstep on every wave.
-// Work is dealt out stream-K over (256-query block, key tile) in equal ranges, one block per CU; a query
-// block cut between blocks is folded by the last arriver (sk_handoff_fwd).  Numerics as fwd_segment's
-// (fp32 row sums of the unrounded weights, FWD_TAU lazy rescale, query pre-scaled by 1/8).
-constexpr int PP_S = 4;                   // K + V ring stages: tile u + 2 is issued while tile u is consumed
-constexpr int PP_STAGE = 2 * TILE_B;      // 16 KB: K tile then V tile
-constexpr int PP_QPB = 256;               // queries per block unit (8 waves x 32)
-
-template <int IMM>
-__device__ __forceinline__ bf16x8 ds_read128_nw(unsigned addr) {
-  bf16x8 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(IMM));
-  return r;
-}
-
-// ring stage PP_S - 1 zeroed once per block before its first walk segment: the t = 0 MFMA phase multiplies that
-// stage (as tile -1) by zero operands, which must not meet NaN bit patterns in uninitialised LDS
-__device__ __forceinline__ void pp_zero_last_stage(char* smem) {
-  uint4* p = reinterpret_cast<uint4*>(smem + (PP_S - 1) * PP_STAGE);
-#pragma unroll
-  for (int i = threadIdx.x; i < PP_STAGE / 16; i += 512) p[i] = make_uint4(0, 0, 0, 0);
-}
-
-struct PpState {
-  bf16x8 qf[4];
-  f32x16 oacc[2], sacc[2];
-  bf16x8 pf[4];
-  float m, l;
-};
-
-// MFMA phase of tile t: QK of tile t (stage KST) and PV of tile t - 1 (stage VST); QK / PV present or not.
-// LDS reads by asm in consumption order, at most 12 in flight (lgkmcnt counts to 15), each group waited
-// for just before its MFMAs: K rows of key half 0 / 1, then the V^T k-slices 0..3 (2 fragments each).
-template <bool QK, bool PV, int KST, int VST>
-__device__ __forceinline__ void pp_mfma(PpState& w, const unsigned (&ka)[4], const unsigned (&va)[2][2]) {
-  // key half b adds 4096 B and a V^T k-slice 2048 B (the swizzle depends on row bits 1-3 only): immediates
-  constexpr int KI = KST * PP_STAGE;
-  constexpr int VI = VST * PP_STAGE + TILE_B;
-  bf16x8 kf[2][4], vf[4][2];
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  auto vread = [&](auto S) __attribute__((always_inline)) {
-    constexpr int s = decltype(S)::value;
-    vf[s][0] = trans_frag_nw<VI + 2048 * s>(va[0][0], va[0][1]);
-    vf[s][1] = trans_frag_nw<VI + 2048 * s>(va[1][0], va[1][1]);
-  };
-  auto kread = [&](auto B) __attribute__((always_inline)) {
-    constexpr int b = decltype(B)::value;
-    kf[b][0] = ds_read128_nw<KI + 4096 * b>(ka[0]);
-    kf[b][1] = ds_read128_nw<KI + 4096 * b>(ka[1]);
-    kf[b][2] = ds_read128_nw<KI + 4096 * b>(ka[2]);
-    kf[b][3] = ds_read128_nw<KI + 4096 * b>(ka[3]);
-  };
-  auto qk = [&](int b) __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w.sacc[b][r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      w.sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[b][s], w.qf[s], w.sacc[b], 0, 0, 0);
-  };
-  auto pv = [&](int s) __attribute__((always_inline)) {
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-      w.oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], w.pf[s], w.oacc[db], 0, 0, 0);
-  };
-  if constexpr (QK) {
-    kread(I0{});
-    kread(I1{});
-  }
-  if constexpr (QK && PV) {
-    vread(I0{});                                                  // K0 K1 V0 in flight
-    lgkm_wait<8>(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
-    qk(0);
-    vread(I1{});                                                  // K1 V0 V1
-    lgkm_wait<8>(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
-    qk(1);
-    vread(I2{});                                                  // V0 V1 V2
-  } else if constexpr (QK) {
-    lgkm_wait<4>(kf[0][0], kf[0][1], kf[0][2], kf[0][3]);
-    qk(0);
-    lgkm_wait<0>(kf[1][0], kf[1][1], kf[1][2], kf[1][3]);
-    qk(1);
-  } else {
-    vread(I0{});
-    vread(I1{});
-    vread(I2{});
-  }
-  if constexpr (PV) {
-    lgkm_wait<8>(vf[0][0], vf[0][1]);
-    pv(0);
-    vread(I3{});                                                  // V1 V2 V3
-    lgkm_wait<8>(vf[1][0], vf[1][1]);
-    pv(1);
-    lgkm_wait<4>(vf[2][0], vf[2][1]);
-    pv(2);
-    lgkm_wait<0>(vf[3][0], vf[3][1]);
-    pv(3);
-  }
-}
-
-// VALU phase of key tile kt: masked tail, row max, lazy rescale of (O, l), exp2, fp32 row sum, P -> bf16.
-// S stays read-only here (the weights go to temporaries): an in-place update makes S a value that differs
-// between the two halves' paths through a segment, and the merge then costs 32 register copies per segment.
-__device__ __forceinline__ void pp_softmax(PpState& w, int kt, int T, int hh) {
-  const bool tail = (kt + 1) * 64 > T;   // keys beyond T exist only in the last tile
-  float mx;
-  if (!tail) {
-    float mx0 = max3_raw(w.sacc[0][0], w.sacc[0][1], w.sacc[0][2]);
-    float mx1 = max3_raw(w.sacc[1][0], w.sacc[1][1], w.sacc[1][2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) {
-      mx0 = max3_raw(mx0, w.sacc[0][r], w.sacc[0][r + 1]);
-      mx1 = max3_raw(mx1, w.sacc[1][r], w.sacc[1][r + 1]);
-    }
-    mx = max3_raw(max3_raw(mx0, mx1, w.sacc[0][15]), w.sacc[1][15], w.sacc[1][15]);
-  } else {
-    mx = -INFINITY;
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        mx = max3_raw(mx, key < T ? w.sacc[b][r] : -INFINITY, mx);
-      }
-  }
-  mx = rowmax_pair(mx);
-  if (__any(mx > w.m + FWD_TAU)) {
-    const float mnew = fmaxf(w.m, mx);
-    const float alpha = fast_exp2((w.m - mnew) * LOG2E);
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) w.oacc[db][r] *= alpha;
-    w.l *= alpha;
-    w.m = mnew;
-  }
-  const float ml = w.m * LOG2E;
-  float p[2][16];
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) p[b][r] = fast_exp2(fmaf(w.sacc[b][r], LOG2E, -ml));
-  if (tail) {
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) p[b][r] = 0.0f;
-  }
-  float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ps[(b << 1) | (r & 1)] += p[b][r];
-  w.l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) w.pf[s][j] = (bf16)p[s >> 1][8 * (s & 1) + j];
-}
-
-// The segment schedule shared by the ping-pong kernels (attn_fwd_pp_kernel, attn_bwd_dq_pp_kernel).  A walk
-// segment of nt key tiles is nt * NB steps (NB parts per tile).  Segment s: half A runs the MFMA phase of step
-// s / 2 when s is even and the VALU phase of step (s - 1) / 2 when s is odd; half B the same one segment later.
-// F::mfma<KST, VST, P, PP>(j) is the MFMA phase of step j (its tile in ring stage KST, part P) with the
-// dependent products of step j - 1 (stage VST, part PP); j == nt NB: only step j - 1's part.  F::valu(j) is the
-// VALU phase of step j.  Ring: tile u + 2 is issued (issue(u), stage u % PP_S) in the segment of A's first
-// step of tile u, after B's last read of tile u - 2 (its dependent products of the last step of tile u - 2,
-// one segment earlier), and waited for before A's first step of tile u + 2; NV = LDS-DMA instructions per tile
-// of the wave (vmcnt of one younger tile).
-template <int NV, int NB, int H, typename F, typename I>
-__device__ __forceinline__ void pp_drive_half(F& f, I&& issue, int nt) {
-  issue(0);
-  if (nt > 1) {
-    issue(1);
-    vm_wait_n<NV>();
-  } else {
-    vm_wait_n<0>();
-  }
-  __syncthreads();
-  const int nst = nt * NB;
-  const int nseg = 2 * nst + 2;
-  auto segment = [&](int s, auto CC) __attribute__((always_inline)) {
-    constexpr int c = decltype(CC)::value;   // s % (8 NB): ring stages and parts are compile-time per copy
-    constexpr int JA = c / 2, JB = (c - 1) / 2;               // A's / B's step mod 4 NB (MFMA copies)
-    constexpr int JAP = (JA + 4 * NB - 1) % (4 * NB), JBP = (JB + 4 * NB - 1) % (4 * NB);
-    if (s >= nseg) return;
-    if constexpr ((c & 1) == 0 && JA % NB == 0) {
-      if (s / (2 * NB) + 2 < nt) issue(s / (2 * NB) + 2);
-    }
-    if constexpr (H == 0) {
-      if constexpr ((c & 1) == 0) f.template mfma<JA / NB, JAP / NB, JA % NB, JAP % NB>(s / 2);
-      else if ((s - 1) / 2 < nst) f.valu((s - 1) / 2);
-    } else {
-      if constexpr ((c & 1) == 1) f.template mfma<JB / NB, JBP / NB, JB % NB, JBP % NB>((s - 1) / 2);
-      else if (s >= 2) f.valu((s - 2) / 2);
-    }
-    if constexpr ((c & 1) == 1 && ((c + 1) / 2) % NB == 0) {
-      // tile (s + 1) / (2 NB), A's next step, landed; the tile after it may stay in flight
-      if ((s + 1) / (2 * NB) + 1 < nt) vm_wait_n<NV>();
-      else vm_wait_n<0>();
-    }
-    __syncthreads();
-  };
-  auto run8 = [&](int s0, auto OFF) __attribute__((always_inline)) {
-    constexpr int o = decltype(OFF)::value;
-    segment(s0 + o, std::integral_constant<int, o>{});
-    segment(s0 + o + 1, std::integral_constant<int, o + 1>{});
-    segment(s0 + o + 2, std::integral_constant<int, o + 2>{});
-    segment(s0 + o + 3, std::integral_constant<int, o + 3>{});
-    segment(s0 + o + 4, std::integral_constant<int, o + 4>{});
-    segment(s0 + o + 5, std::integral_constant<int, o + 5>{});
-    segment(s0 + o + 6, std::integral_constant<int, o + 6>{});
-    segment(s0 + o + 7, std::integral_constant<int, o + 7>{});
-  };
-  for (int s0 = 0; s0 < nseg; s0 += 8 * NB) {
-    run8(s0, std::integral_constant<int, 0>{});
-    if constexpr (NB == 2) run8(s0, std::integral_constant<int, 8>{});
-  }
-}
-
-// each half runs its own copy of the segment loop (same barrier sequence): no per-segment branch on the half, so
-// the values carried between a wave's phases have one definition per program point (no merge copies)
-template <int NV, int NB, typename F, typename I>
-__device__ __forceinline__ void pp_drive(F& f, I&& issue, int nt, int half) {
-  if (half == 0) pp_drive_half<NV, NB, 0>(f, issue, nt);
-  else pp_drive_half<NV, NB, 1>(f, issue, nt);
-}
-
-struct FwdPpOps {
-  PpState& w;
-  const unsigned (&ka)[4];
-  const unsigned (&va)[2][2];
-  int nt, t0, T, hh;
-  // one body for every tile: at t = 0 the PV part multiplies the zeroed ring stage by P = 0, at t = nt the QK
-  // part reads a stale stage whose S is never used (no per-tile variants: their merges cost register copies)
-  template <int KST, int VST, int P, int PP>
-  __device__ __forceinline__ void mfma(int) { pp_mfma<true, true, KST, VST>(w, ka, va); }
-  __device__ __forceinline__ void valu(int t) { pp_softmax(w, t0 + t, T, hh); }
-};
-
-__device__ __forceinline__ void fwd_pp_segment(char* smem, const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo,
-                                               float* lse, int qbk, int h, int n, int t0, int nt, const AttnSK& sk,
-                                               long bi, int seg, bool whole) {
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int wid = threadIdx.x >> 6;
-  const int half = __builtin_amdgcn_readfirstlane(wid >> 2);   // 0: A, 1: B (one segment behind)
-  const int C = heads * 64;
-  const bf16* base = qkv + (long)n * T * ld;
-  const int my_q = qbk * PP_QPB + wid * 32 + (lane & 31);
-  const bool qok = my_q < T;
-  PpState w;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) w.qf[s] = load_row8(base + (long)my_q * ld + h * 64 + 16 * s + 8 * hh, qok, 0.125f);
-  w.m = -INFINITY;
-  w.l = 0.0f;
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w.oacc[db][r] = 0.0f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) w.pf[s] = bf16x8{};   // tile -1's P: the first PV adds nothing
-
-  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
-  const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
-  TileDma<512> dma;
-  dma.init(threadIdx.x, ld);
-  auto issue = [&](int u) __attribute__((always_inline)) {
-    char* st = smem + (u % PP_S) * PP_STAGE;
-    dma.issue(rk, st, (t0 + u) * 64, T, ld, threadIdx.x);
-    dma.issue(rv, st + TILE_B, (t0 + u) * 64, T, ld, threadIdx.x);
-  };
-  const unsigned sb = lds_addr(smem);
-  unsigned ka[4], va[2][2];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) ka[s] = sb + row_off(lane & 31, 2 * s + hh);
-#pragma unroll
-  for (int db = 0; db < 2; ++db) {
-    const TrOff t = tr_off(0, 32 * db, lane);
-    va[db][0] = sb + t.lo;
-    va[db][1] = sb + t.hi;
-  }
-  FwdPpOps ops{w, ka, va, nt, t0, T, hh};
-  pp_drive<2, 1>(ops, issue, nt, half);
-  float m = w.m, l = w.l + __shfl_xor(w.l, 32, 64);
-  if (!whole) {   // query block shared with other blocks: merge (m, l, O) in block order
-    float v[34];
-    v[0] = m;
-    v[1] = l;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[2 + 16 * db + r] = w.oacc[db][r];
-    if (!sk_handoff_fwd<8>(sk, smem, bi, (T + 63) / 64, seg, v)) return;
-    m = v[0];
-    l = v[1];
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) w.oacc[db][r] = v[2 + 16 * db + r];
-  }
-  const float inv = 1.0f / l;
-  if (qok) {
-    bf16* orow = o + ((long)n * T + my_q) * ldo + h * 64;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int g2 = 0; g2 < 4; ++g2) {
-        bf16x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (bf16)(w.oacc[db][4 * g2 + e] * inv);
-        *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * g2 + 4 * hh) = v;
-      }
-    if (hh == 0) lse[((long)n * heads + h) * T + my_q] = m + logf(l);
-  }
-}
-
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_fwd_pp_kernel(
-    const bf16* qkv, int ld, int T, int heads, bf16* o, int ldo, float* lse, AttnSK sk) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_S * PP_STAGE];
-  const int ntk = (T + 63) / 64;
-  const int nqb = (T + PP_QPB - 1) / PP_QPB;
-  pp_zero_last_stage(smem);   // (made visible by the first walk segment's prologue barrier)
-  sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
-    const int qbk = (int)(bi % nqb);
-    const long nh = bi / nqb;
-    fwd_pp_segment(smem, qkv, ld, T, heads, o, ldo, lse, qbk, (int)(nh % heads), (int)(nh / heads), t0, cnt, sk, bi,
-                   seg, t0 == 0 && cnt == ntk);
-  });
+  fwd_segment<QW, KS>(smem, qkv, ld, T, heads, o, ldo, lse, blockIdx.x, blockIdx.y, blockIdx.z, 0, (T + 63) / 64);
 }
 
 // ------------------------------------------------------------------------------ backward
@@ -1464,442 +1009,9 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 }
 
 
-// -------------------------------------------------------------------------------- dQ, ping-pong
-// pp_drive's schedule for dQ, two steps per key tile (32 keys each, to fit two waves' registers per SIMD):
-// 8-wave blocks, 32 queries per wave resident (Q, dO fragments, lse, delta), K / V tiles through the shared
-// ring.  MFMA phase of step j: S^T = K Q^T and dP^T = V dO^T of its 32 keys, dQ^T += K^T dS^T of step j - 1
-// (12 MFMAs); VALU phase: P = exp2(S log2e - lse), dS = P (dP - delta), tail keys masked, dS packed to bf16.
-// Stream-K over (256-query block, key tile), partial dQ summed in block order by the last arriver
-// (sk_handoff); delta published by the segment that starts at key 0 (the dK/dV kernel runs next).
-struct DqPpState {
-  bf16x8 qf[4], df[4];
-  f32x16 sacc, dpacc, dq[2];
-  bf16x8 sf[2];   // dS^T of the previous step by k-slice
-  float lse2, del;
-};
-
-// LDS reads by asm in consumption order, at most 12 in flight: K rows / V rows of the step's key half (tile
-// stage KST, half P), then the K^T fragments of step j - 1 (stage VST, half PP) by k-slice.  A key half adds
-// 32 rows (4096 B), a k-slice 16 rows (2048 B); the swizzle depends on row bits 1-3 only, so both offsets are
-// immediates on 4 + 4 per-lane base addresses.
-template <bool QK, bool DQ, int KST, int VST, int P, int PP>
-__device__ __forceinline__ void dqpp_mfma(DqPpState& w, const unsigned (&ka)[4], const unsigned (&ta)[2][2]) {
-  constexpr int KI = KST * PP_STAGE + 4096 * P, VI = KI + TILE_B, TI = VST * PP_STAGE + 4096 * PP;
-  bf16x8 kf[4], vf[4], fq[2][2];
-  auto rk = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kf[s] = ds_read128_nw<KI>(ka[s]);
-  };
-  auto rv = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) vf[s] = ds_read128_nw<VI>(ka[s]);
-  };
-  auto rt0 = [&]() __attribute__((always_inline)) {
-    fq[0][0] = trans_frag_nw<TI>(ta[0][0], ta[0][1]);
-    fq[0][1] = trans_frag_nw<TI>(ta[1][0], ta[1][1]);
-  };
-  auto rt1 = [&]() __attribute__((always_inline)) {
-    fq[1][0] = trans_frag_nw<TI + 2048>(ta[0][0], ta[0][1]);
-    fq[1][1] = trans_frag_nw<TI + 2048>(ta[1][0], ta[1][1]);
-  };
-  auto mk = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w.sacc[r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) w.sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[s], w.qf[s], w.sacc, 0, 0, 0);
-  };
-  auto mv = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w.dpacc[r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) w.dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s], w.df[s], w.dpacc, 0, 0, 0);
-  };
-  auto mt = [&](int s2) __attribute__((always_inline)) {
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-      w.dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fq[s2][db], w.sf[s2], w.dq[db], 0, 0, 0);
-  };
-  if constexpr (QK && DQ) {
-    rk(); rv(); rt0();
-    lgkm_wait<8>(kf[0], kf[1], kf[2], kf[3]); mk(); rt1();
-    lgkm_wait<8>(vf[0], vf[1], vf[2], vf[3]); mv();
-    lgkm_wait<4>(fq[0][0], fq[0][1]); mt(0);
-    lgkm_wait<0>(fq[1][0], fq[1][1]); mt(1);
-  } else if constexpr (QK) {
-    rk(); rv();
-    lgkm_wait<4>(kf[0], kf[1], kf[2], kf[3]); mk();
-    lgkm_wait<0>(vf[0], vf[1], vf[2], vf[3]); mv();
-  } else {
-    rt0(); rt1();
-    lgkm_wait<4>(fq[0][0], fq[0][1]); mt(0);
-    lgkm_wait<0>(fq[1][0], fq[1][1]); mt(1);
-  }
-}
-
-struct DqPpOps {
-  DqPpState& w;
-  const unsigned (&ka)[4];
-  const unsigned (&ta)[2][2];
-  int nst, t0, T, hh;
-  template <int KST, int VST, int P, int PP>
-  __device__ __forceinline__ void mfma(int) { dqpp_mfma<true, true, KST, VST, P, PP>(w, ka, ta); }   // as FwdPpOps
-  __device__ __forceinline__ void valu(int j) {
-    const int k0 = (t0 + (j >> 1)) * 64 + 32 * (j & 1);   // first key of the step
-    float ds[16];   // dS^T in temporaries (S / dP stay read-only: see pp_softmax)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float pv = fast_exp2(fmaf(w.sacc[r], LOG2E, -w.lse2));
-      ds[r] = pv * (w.dpacc[r] - w.del);
-    }
-    if (k0 + 32 > T) {  // keys beyond T exist only in the last tile
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (k0 + (r & 3) + 8 * (r >> 2) + 4 * hh >= T) ds[r] = 0.0f;
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) w.sf[s2][e] = (bf16)ds[8 * s2 + e];
-  }
-};
-
-__device__ __forceinline__ void dq_pp_segment(char* smem, const bf16* qkv, int ld, const bf16* o, int ldo,
-                                              const bf16* dout, int lddo, const float* lse, float* delta, int T,
-                                              int heads, bf16* dqkv, int ldd, int qbk, int h, int n, int t0, int nt,
-                                              const AttnSK& sk, long bi, int seg, bool whole) {
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int wid = threadIdx.x >> 6;
-  const int half = __builtin_amdgcn_readfirstlane(wid >> 2);
-  const int C = heads * 64;
-  const bf16* base = qkv + (long)n * T * ld;
-  const int my_q = qbk * PP_QPB + wid * 32 + (lane & 31);
-  const bool qok = my_q < T;
-  DqPpState w;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    w.qf[s] = load_row8(base + (long)my_q * ld + h * 64 + 16 * s + 8 * hh, qok, 0.125f);
-    w.df[s] = load_row8(dout + ((long)n * T + my_q) * lddo + h * 64 + 16 * s + 8 * hh, qok, 1.0f);
-  }
-  w.lse2 = qok ? lse[((long)n * heads + h) * T + my_q] * LOG2E : INFINITY;
-  // delta = sum_d dO * O (fp32, fixed order), as dq_segment
-  float my_del = 0.0f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const bf16x8 of = load_row8(o + ((long)n * T + my_q) * ldo + h * 64 + 16 * s + 8 * hh, qok, 1.0f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) my_del = fmaf((float)w.df[s][j], (float)of[j], my_del);
-  }
-  my_del += __shfl_xor(my_del, 32, 64);
-  w.del = my_del;
-  w.sf[0] = bf16x8{};   // step -1's dS: the first dQ product adds nothing
-  w.sf[1] = bf16x8{};
-  if (qok && hh == 0 && t0 == 0) delta[((long)n * heads + h) * T + my_q] = my_del;
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w.dq[db][r] = 0.0f;
-
-  const __amdgpu_buffer_rsrc_t rk = buf_rsrc(base + C + h * 64);
-  const __amdgpu_buffer_rsrc_t rv = buf_rsrc(base + 2 * C + h * 64);
-  TileDma<512> dma;
-  dma.init(threadIdx.x, ld);
-  auto issue = [&](int u) __attribute__((always_inline)) {
-    char* st = smem + (u % PP_S) * PP_STAGE;
-    dma.issue(rk, st, (t0 + u) * 64, T, ld, threadIdx.x);
-    dma.issue(rv, st + TILE_B, (t0 + u) * 64, T, ld, threadIdx.x);
-  };
-  const unsigned sb = lds_addr(smem);
-  unsigned ka[4], ta[2][2];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) ka[s] = sb + row_off(lane & 31, 2 * s + hh);
-#pragma unroll
-  for (int db = 0; db < 2; ++db) {
-    const TrOff t = tr_off(0, 32 * db, lane);
-    ta[db][0] = sb + t.lo;
-    ta[db][1] = sb + t.hi;
-  }
-  DqPpOps ops{w, ka, ta, 2 * nt, t0, T, hh};
-  pp_drive<2, 2>(ops, issue, nt, half);
-  if (!whole) {
-    float v[32];
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[16 * db + r] = w.dq[db][r];
-    if (!sk_handoff<8, 32>(sk, smem, bi, (T + 63) / 64, seg, v)) return;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) w.dq[db][r] = v[16 * db + r];
-  }
-  if (qok) {
-    bf16* row = dqkv + ((long)n * T + my_q) * ldd + h * 64;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int g2 = 0; g2 < 4; ++g2) {
-        bf16x4 a;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] = (bf16)(w.dq[db][4 * g2 + e] * 0.125f);
-        *reinterpret_cast<bf16x4*>(row + 32 * db + 8 * g2 + 4 * hh) = a;
-      }
-  }
-}
-
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_pp_kernel(
-    const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse, float* delta,
-    int T, int heads, bf16* dqkv, int ldd, AttnSK sk) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_S * PP_STAGE];
-  const int ntk = (T + 63) / 64;
-  const int nqb = (T + PP_QPB - 1) / PP_QPB;
-  pp_zero_last_stage(smem);   // (made visible by the first walk segment's prologue barrier)
-  sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
-    const int qbk = (int)(bi % nqb);
-    const long nh = bi / nqb;
-    dq_pp_segment(smem, qkv, ld, o, ldo, dout, lddo, lse, delta, T, heads, dqkv, ldd, qbk, (int)(nh % heads),
-                  (int)(nh / heads), t0, cnt, sk, bi, seg, t0 == 0 && cnt == ntk);
-  });
-}
-
-// ------------------------------------------------------------------------------ dK/dV, ping-pong
-// pp_drive's schedule for dK/dV, two 32-query steps per tile: 8-wave blocks, 32 keys per wave resident (K, V
-// fragments; dK^T, dV^T accumulators), Q / dO tiles through the shared ring, their lse / delta rows in a small
-// ring of their own.  MFMA phase of step j: S = Q K^T and dP = dO V^T of its 32 queries (8 MFMAs), dV^T += dO^T
-// P and dK^T += Q^T dS of step j - 1 (8 MFMAs); VALU phase: P = exp2(S log2e / 8 - lse log2e), dS = P (dP -
-// delta), both packed to bf16.  Queries beyond T have zero Q / dO / lse / delta rows, so they add nothing.
-// Stream-K over (256-key block, query tile), partial dK / dV summed in block order by the last arriver.
-constexpr int PPB_LSE = PP_S * PP_STAGE;   // [stage][lse 64 | delta 64] fp32 after the Q / dO ring
-
-struct DkdvPpState {
-  bf16x8 kf[4], vf[4];
-  f32x16 dk[2], dv[2];
-  f32x16 sp, dp;
-  bf16x8 pf[2], sf[2];   // P / dS of the previous step by k-slice
-};
-
-// LDS reads by asm in consumption order, at most 12 in flight: Q rows / dO rows of the step's query half (stage
-// KST, half P), then the dO^T and Q^T fragments of step j - 1 (stage VST, half PP) by k-slice
-template <bool QK, bool DKV, int KST, int VST, int P, int PP>
-__device__ __forceinline__ void dkdvpp_mfma(DkdvPpState& w, const unsigned (&qa)[4], const unsigned (&ta)[2][2]) {
-  constexpr int QI = KST * PP_STAGE + 4096 * P, DI = QI + TILE_B;
-  constexpr int TQ = VST * PP_STAGE + 4096 * PP, TD = TQ + TILE_B;
-  bf16x8 qr[4], dr[4], fv[2][2], fk[2][2];
-  auto rq = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qr[s] = ds_read128_nw<QI>(qa[s]);
-  };
-  auto rd = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) dr[s] = ds_read128_nw<DI>(qa[s]);
-  };
-  auto rfv = [&](auto S2) __attribute__((always_inline)) {
-    constexpr int s2 = decltype(S2)::value;
-    fv[s2][0] = trans_frag_nw<TD + 2048 * s2>(ta[0][0], ta[0][1]);
-    fv[s2][1] = trans_frag_nw<TD + 2048 * s2>(ta[1][0], ta[1][1]);
-  };
-  auto rfk = [&](auto S2) __attribute__((always_inline)) {
-    constexpr int s2 = decltype(S2)::value;
-    fk[s2][0] = trans_frag_nw<TQ + 2048 * s2>(ta[0][0], ta[0][1]);
-    fk[s2][1] = trans_frag_nw<TQ + 2048 * s2>(ta[1][0], ta[1][1]);
-  };
-  auto ms = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w.sp[r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) w.sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr[s], w.kf[s], w.sp, 0, 0, 0);
-  };
-  auto md = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) w.dp[r] = 0.0f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) w.dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dr[s], w.vf[s], w.dp, 0, 0, 0);
-  };
-  auto mdv = [&](int s2) __attribute__((always_inline)) {
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-      w.dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fv[s2][db], w.pf[s2], w.dv[db], 0, 0, 0);
-  };
-  auto mdk = [&](int s2) __attribute__((always_inline)) {
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-      w.dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk[s2][db], w.sf[s2], w.dk[db], 0, 0, 0);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  if constexpr (QK && DKV) {
-    rq(); rd(); rfv(I0{});
-    lgkm_wait<8>(qr[0], qr[1], qr[2], qr[3]); ms(); rfk(I0{});
-    lgkm_wait<8>(dr[0], dr[1], dr[2], dr[3]); md(); rfv(I1{});
-    lgkm_wait<8>(fv[0][0], fv[0][1]); mdv(0); rfk(I1{});
-    lgkm_wait<8>(fk[0][0], fk[0][1]); mdk(0);
-    lgkm_wait<4>(fv[1][0], fv[1][1]); mdv(1);
-    lgkm_wait<0>(fk[1][0], fk[1][1]); mdk(1);
-  } else if constexpr (QK) {
-    rq(); rd();
-    lgkm_wait<4>(qr[0], qr[1], qr[2], qr[3]); ms();
-    lgkm_wait<0>(dr[0], dr[1], dr[2], dr[3]); md();
-  } else {
-    rfv(I0{}); rfk(I0{}); rfv(I1{});
-    lgkm_wait<8>(fv[0][0], fv[0][1]); mdv(0); rfk(I1{});
-    lgkm_wait<8>(fk[0][0], fk[0][1]); mdk(0);
-    lgkm_wait<4>(fv[1][0], fv[1][1]); mdv(1);
-    lgkm_wait<0>(fk[1][0], fk[1][1]); mdk(1);
-  }
-}
-
-struct DkdvPpOps {
-  DkdvPpState& w;
-  const unsigned (&qa)[4];
-  const unsigned (&ta)[2][2];
-  const char* lsb;   // lse / delta ring
-  int nst, hh;
-  template <int KST, int VST, int P, int PP>
-  __device__ __forceinline__ void mfma(int) { dkdvpp_mfma<true, true, KST, VST, P, PP>(w, qa, ta); }   // as FwdPpOps
-  __device__ __forceinline__ void valu(int j) {
-    constexpr float L8 = LOG2E * 0.125f;
-    // accumulator element r holds query 32 (j & 1) + 8 (r >> 2) + 4 hh + (r & 3) of the tile
-    const float* ls = reinterpret_cast<const float*>(lsb + ((j >> 1) % PP_S) * 512) + 32 * (j & 1) + 4 * hh;
-    const float* dl = ls + 64;
-    float pv[16], ds[16];   // P / dS in temporaries (S / dP stay read-only: see pp_softmax)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + 8 * g);
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + 8 * g);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        pv[4 * g + e] = fast_exp2(fmaf(w.sp[4 * g + e], L8, -l4[e] * LOG2E));
-        ds[4 * g + e] = pv[4 * g + e] * (w.dp[4 * g + e] - d4[e]);
-      }
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        w.pf[s2][e] = (bf16)pv[8 * s2 + e];
-        w.sf[s2][e] = (bf16)ds[8 * s2 + e];
-      }
-  }
-};
-
-__device__ __forceinline__ void dkdv_pp_segment(char* smem, const bf16* qkv, int ld, const bf16* dout, int lddo,
-                                                const float* lse, const float* delta, int T, int heads, bf16* dqkv,
-                                                int ldd, int kb, int h, int n, int t0, int nt, const AttnSK& sk,
-                                                long bi, int seg, bool whole) {
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  const int wid = threadIdx.x >> 6;
-  const int half = __builtin_amdgcn_readfirstlane(wid >> 2);
-  const int C = heads * 64;
-  const bf16* base = qkv + (long)n * T * ld;
-  const bf16* dob = dout + (long)n * T * lddo;
-  const int my_k = kb * PP_QPB + wid * 32 + (lane & 31);
-  const bool kok = my_k < T;
-  DkdvPpState w;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    w.kf[s] = load_row8(base + (long)my_k * ld + C + h * 64 + 16 * s + 8 * hh, kok, 1.0f);
-    w.vf[s] = load_row8(base + (long)my_k * ld + 2 * C + h * 64 + 16 * s + 8 * hh, kok, 1.0f);
-  }
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      w.dk[db][r] = 0.0f;
-      w.dv[db][r] = 0.0f;
-    }
-  w.pf[0] = w.pf[1] = w.sf[0] = w.sf[1] = bf16x8{};   // step -1's P / dS: the first products add nothing
-  const __amdgpu_buffer_rsrc_t rq = buf_rsrc(base + h * 64);
-  const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dob + h * 64);
-  const __amdgpu_buffer_rsrc_t rl = buf_rsrc(lse + ((long)n * heads + h) * T);
-  const __amdgpu_buffer_rsrc_t rdl = buf_rsrc(delta + ((long)n * heads + h) * T);
-  TileDma<512> q_dma, d_dma;
-  q_dma.init(threadIdx.x, ld);
-  d_dma.init(threadIdx.x, lddo);
-  const int wv = __builtin_amdgcn_readfirstlane(wid);
-  char* lsb = smem + PPB_LSE;
-  auto issue = [&](int u) __attribute__((always_inline)) {
-    char* st = smem + (u % PP_S) * PP_STAGE;
-    const int r0 = (t0 + u) * 64;
-    q_dma.issue(rq, st, r0, T, ld, threadIdx.x);
-    d_dma.issue(rd, st + TILE_B, r0, T, lddo, threadIdx.x);
-    if (wv == 0) {  // lse / delta rows of the tile (rows >= T read 0)
-      const int soff = __builtin_amdgcn_readfirstlane(r0 * 4);
-      char* ls = lsb + (u % PP_S) * 512;
-      buf_load_lds4(rl, (DC_LDS char*)ls, r0 + lane < T ? lane * 4 : kOOB, soff);
-      buf_load_lds4(rdl, (DC_LDS char*)ls + 256, r0 + lane < T ? lane * 4 : kOOB, soff);
-    }
-  };
-  const unsigned sb = lds_addr(smem);
-  unsigned qa[4], ta[2][2];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) qa[s] = sb + row_off(lane & 31, 2 * s + hh);
-#pragma unroll
-  for (int db = 0; db < 2; ++db) {
-    const TrOff t = tr_off(0, 32 * db, lane);
-    ta[db][0] = sb + t.lo;
-    ta[db][1] = sb + t.hi;
-  }
-  DkdvPpOps ops{w, qa, ta, lsb, 2 * nt, hh};
-  pp_drive<2, 2>(ops, issue, nt, half);   // (wave 0 has 4 instructions per tile: vmcnt(2) over-waits, safely)
-  if (!whole) {
-    float v[64];
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        v[16 * db + r] = w.dk[db][r];
-        v[32 + 16 * db + r] = w.dv[db][r];
-      }
-    if (!sk_handoff<8, 64>(sk, smem, bi, (T + 63) / 64, seg, v)) return;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        w.dk[db][r] = v[16 * db + r];
-        w.dv[db][r] = v[32 + 16 * db + r];
-      }
-  }
-  if (kok) {
-    bf16* row = dqkv + ((long)n * T + my_k) * ldd;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int g2 = 0; g2 < 4; ++g2) {
-        bf16x4 a, b;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          a[e] = (bf16)(w.dk[db][4 * g2 + e] * 0.125f);  // dK = dS^T (Q / 8)
-          b[e] = (bf16)w.dv[db][4 * g2 + e];
-        }
-        const int d = 32 * db + 8 * g2 + 4 * hh;
-        *reinterpret_cast<bf16x4*>(row + C + h * 64 + d) = a;
-        *reinterpret_cast<bf16x4*>(row + 2 * C + h * 64 + d) = b;
-      }
-  }
-}
-
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_pp_kernel(
-    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
-    bf16* dqkv, int ldd, AttnSK sk) {
-  __shared__ __attribute__((aligned(16))) char smem[PPB_LSE + PP_S * 512];
-  const int ntq = (T + 63) / 64;
-  const int nkb = (T + PP_QPB - 1) / PP_QPB;
-  pp_zero_last_stage(smem);   // (made visible by the first walk segment's prologue barrier)
-  sk_walk(sk, ntq, [&](long bi, int t0, int cnt, int seg) {
-    const int kb = (int)(bi % nkb);
-    const long nh = bi / nkb;
-    dkdv_pp_segment(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, kb, (int)(nh % heads),
-                    (int)(nh / heads), t0, cnt, sk, bi, seg, t0 == 0 && cnt == ntq);
-  });
-}
 }  // namespace
 
 namespace {
-// forward softmax with the lazy rescale decided from the row sum (fwd_segment FS); DC_ATTN_FASTSM=0 / 1
-bool fast_softmax() {
-  const char* e = getenv("DC_ATTN_FASTSM");   // read per launch (host side, once per captured graph node)
-  return e && atoi(e) != 0;
-}
-
 // (query waves per block, key splits per block): chosen per launch by a makespan model over the
 // 256 CUs -- rounds of blocks x per-block work (QW) -- discounted when fewer than 8 waves are
 // resident per CU.  DC_ATTN_CFG=<index> forces one (tests / benchmarks).
@@ -1936,13 +1048,7 @@ int attn_cfg(int t, int heads, int nb, bool bwd) {
 template <int QW, int KS>
 void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
-  const AttnSK none{};
-  if (fast_softmax())
-    hipLaunchKernelGGL((attn_fwd_kernel<QW, KS, false, true>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o,
-                       ldo, lse, none);
-  else
-    hipLaunchKernelGGL((attn_fwd_kernel<QW, KS, false, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o,
-                       ldo, lse, none);
+  hipLaunchKernelGGL((attn_fwd_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o, ldo, lse);
 }
 
 // dQ first: it computes delta = rowsum(dO * O) for its resident queries and publishes it; dK/dV (next
@@ -2013,78 +1119,6 @@ bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* 
   return true;
 }
 
-// Stream-K forward: opt-in (DC_ATTN_SK_FWD=1: the backward's policy, 2: wherever it fits).  Measured
-// neutral at level 0 (108 vs 109 us, C2 unchanged: profiles/r01r_attn_fwd_sk.txt): the forward's plain
-// (5, 2) grid already runs 10-wave blocks, and it is VALU-bound (exp) rather than occupancy-bound.
-bool launch_fwd_sk(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, float* ws,
-                   long ws_bytes, hipStream_t st) {
-  AttnSK sk;
-  const char* on = getenv("DC_ATTN_SK_FWD");
-  if (!on || atoi(on) == 0 || (getenv("DC_ATTN_SK") && atoi(getenv("DC_ATTN_SK")) == 0)) return false;
-  if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK_FWD", sk)) return false;
-  hipLaunchKernelGGL((attn_fwd_kernel<4, 1, true, false>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, t, heads, o,
-                     ldo, lse, sk);
-  return true;
-}
-
-// stream-K plan of the 8-wave ping-pong kernels over (256-query block, key tile): one block per CU; NV fp32
-// partial values per lane and slab slot; false when it does not apply (env: "0" off, "2" wherever it fits)
-bool pp_plan(int t, int heads, int nb, float* ws, long ws_bytes, const char* env_name, int nv, AttnSK& sk) {
-  // opt-in: measured no faster than the one-barrier-per-tile kernels (level 0 fwd 101 vs 104 us, bwd 275 vs 272 us;
-  // slower at levels 1-2, profiles/r04n): both are bound by the softmax's VALU issue, which the phase split does
-  // not shorten
-  const char* env = getenv(env_name);   // read per launch (host side, once per captured graph node)
-  if (!ws || !env || atoi(env) == 0 || getenv("DC_ATTN_CFG")) return false;
-  const bool forced = atoi(env) == 2;
-  const long units = (long)((t + PP_QPB - 1) / PP_QPB) * heads * nb;
-  const int ntile = (t + 63) / 64;
-  const char* ge = getenv("DC_ATTN_PP_G");   // grid size override (experiments)
-  const long G = ge && atoi(ge) > 0 ? atoi(ge) : device_cus();
-  const long U = units * ntile;
-  if (!forced && U < 16 * G) return false;
-  if (units > kAttnCounterBytes / 4) return false;
-  const long g = min(G, U);
-  const int spb = (int)(((U + g - 1) / g + ntile - 1) / ntile + 1);
-  if (g * spb * 8 * nv * 64L * 4 > ws_bytes - kAttnCounterBytes) return false;
-  sk.slab = ws;
-  sk.counters = reinterpret_cast<int*>(reinterpret_cast<char*>(ws) + (ws_bytes - kAttnCounterBytes));
-  sk.U = U;
-  sk.G = (int)g;
-  sk.spb = spb;
-  return true;
-}
-
-// Ping-pong forward (attn_fwd_pp_kernel): one 8-wave block per CU, stream-K over (256-query block, key tile).
-// Opt-in: DC_ATTN_PP=1 wherever every block gets >= 16 key tiles, 2 wherever the slab fits (tests); a forced
-// DC_ATTN_CFG bypasses it.
-bool launch_fwd_pp(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int ldo, float* lse, float* ws,
-                   long ws_bytes, hipStream_t st) {
-  AttnSK sk;
-  if (!pp_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_PP", 34, sk)) return false;
-  hipLaunchKernelGGL(attn_fwd_pp_kernel, dim3((unsigned)sk.G), dim3(512), 0, st, qkv, ld, t, heads, o, ldo, lse, sk);
-  return true;
-}
-
-// Ping-pong dQ (attn_bwd_dq_pp_kernel), same policy as the forward's (DC_ATTN_PP_DQ=1 / 2).
-bool launch_dq_pp(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
-                  float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes,
-                  hipStream_t st) {
-  AttnSK sk;
-  if (!pp_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_PP_DQ", 32, sk)) return false;
-  hipLaunchKernelGGL(attn_bwd_dq_pp_kernel, dim3((unsigned)sk.G), dim3(512), 0, st, qkv, ld, o, ldo, dout, lddo, lse,
-                     delta, t, heads, dqkv, ldd, sk);
-  return true;
-}
-
-// Ping-pong dK/dV (attn_bwd_dkdv_pp_kernel), same policy (DC_ATTN_PP_DKDV=1 / 2).
-bool launch_dkdv_pp(const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int t,
-                    int heads, int nb, bf16* dqkv, int ldd, float* ws, long ws_bytes, hipStream_t st) {
-  AttnSK sk;
-  if (!pp_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_PP_DKDV", 64, sk)) return false;
-  hipLaunchKernelGGL(attn_bwd_dkdv_pp_kernel, dim3((unsigned)sk.G), dim3(512), 0, st, qkv, ld, dout, lddo, lse, delta,
-                     t, heads, dqkv, ldd, sk);
-  return true;
-}
 }  // namespace
 
 extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse,
@@ -2093,11 +1127,8 @@ extern "C" int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, vo
   if (ld % 8 || ldo % 8 || ld < 3 * heads * 64 || ldo < heads * 64) return DC_ERR_ALIGN;
   const bf16* q = (const bf16*)qkv;
   hipStream_t st = (hipStream_t)stream;
-  if (launch_fwd_sk(q, ld, t, heads, nb, (bf16*)o, ldo, lse, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st) ||
-      launch_fwd_pp(q, ld, t, heads, nb, (bf16*)o, ldo, lse, ws, ws_bytes < (1LL << 40) ? (long)ws_bytes : 0, st)) {
-    DC_CHECK_LAUNCH();
-    return DC_OK;
-  }
+  (void)ws;
+  (void)ws_bytes;
   switch (attn_cfg(t, heads, nb, false)) {
     case 0: launch_fwd<4, 1>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
     case 1: launch_fwd<4, 2>(q, ld, t, heads, nb, (bf16*)o, ldo, lse, st); break;
@@ -2120,21 +1151,17 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   const bf16* d = (const bf16*)dout;
   bf16* g = (bf16*)dqkv;
   const long wsb = ws_bytes < (1LL << 40) ? (long)ws_bytes : 0;
-  // dQ first (it publishes delta for dK/dV), then dK/dV: each by its ping-pong kernel where the policy applies,
-  // else by the stream-K or plain-grid kernels
-  auto legacy = [&](bool with_dq, bool with_dkdv) {
-    if (launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, with_dq, with_dkdv, st))
-      return;
+  // dQ first (it publishes delta for dK/dV), then dK/dV: by the stream-K kernels where the plan applies, else on
+  // the plain grid
+  if (!launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, true, true, st)) {
     const int cfg = attn_cfg(t, heads, nb, true);
     if (cfg == 0)
-      launch_bwd<4, 1>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, with_dq, with_dkdv, st);
+      launch_bwd<4, 1>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, true, true, st);
     else if (cfg == 1)
-      launch_bwd<4, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, with_dq, with_dkdv, st);
+      launch_bwd<4, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, true, true, st);
     else
-      launch_bwd<2, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, with_dq, with_dkdv, st);
-  };
-  if (!launch_dq_pp(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, st)) legacy(true, false);
-  if (!launch_dkdv_pp(q, ld, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, st)) legacy(false, true);
+      launch_bwd<2, 2>(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, true, true, st);
+  }
   DC_CHECK_LAUNCH();
   return DC_OK;
 }

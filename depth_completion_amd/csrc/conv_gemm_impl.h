@@ -218,8 +218,12 @@ __device__ __forceinline__ void epilogue_store(const ConvGemmParams& p, long m, 
 // kEpiEarly: load them at kernel start.  Off: holding them across the main loop cost 20-90 VGPRs in most im2col
 // instantiations (128 x 128 x 32: 140 -> 228, 128 x 64 x 64: 144 -> 188) and a wave per SIMD of occupancy, which the
 // runtime A/B (DC_HALO_DIAG=256, same binary) could not show: C3 conv launches +21 % (profiles/r04z).  The epilogue
-// then loads every operand after the main loop (the round-3 placement).
-constexpr bool kEpiEarly = false;
+// then loads every operand after the main loop (the round-3 placement).  Build-time switch, left out of the default
+// build (-DDC_EPI_EARLY=1 compiles the early placement in; DC_HALO_DIAG=256 then selects it per launch).
+#ifndef DC_EPI_EARLY
+#define DC_EPI_EARLY 0
+#endif
+constexpr bool kEpiEarly = DC_EPI_EARLY != 0;
 template <int NJ, int RMAX>
 struct EpiPre {
   float cv[NJ];        // per-column bias (GNM 3: csum)

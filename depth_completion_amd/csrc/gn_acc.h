@@ -1,12 +1,14 @@
-// Exact GroupNorm statistics accumulators (include/dcamd.h dc_gn_fuse), shared by the conv epilogues that add
-// to them (conv_gemm.hip) and the one-pass GroupNorm kernels that read them (norms.hip).
+// Order-independent GroupNorm statistics accumulators (include/dcamd.h dc_gn_fuse), shared by the conv epilogues
+// that add to them (conv_gemm.hip) and the one-pass GroupNorm kernels that read them (norms.hip).
 //
 // A quantity is kGnWords int64 words: 8 limbs of a fixed-point integer whose LSB is 2^-120 (limb j holds bits
 // [32 j, 32 j + 32) of every contribution, with 32 bits of headroom for carries) and a count of non-finite
 // contributions.  A finite fp32 x = m 2^(e - 150) (m the 24-bit significand, e the biased exponent) with e >= 30
 // adds m << (e - 30) to at most two adjacent limbs; |x| < 2^-97 is dropped.  Integer addition commutes, so the
 // accumulated value is the exact sum of the contributions whatever order the tiles arrive in: the statistics are
-// bitwise reproducible without a fixed-order fold (and more accurate than an fp32 tree).
+// bitwise reproducible without a fixed-order fold.  The contributions themselves are not the elements: each block
+// first folds its tile's per-lane / per-channel sums in fp32 (a fixed order, so deterministic, but rounded), and
+// only those block partials are summed exactly -- accurate to the fp32 partials, not exact over the elements.
 #pragma once
 #include "common.h"
 

@@ -648,247 +648,6 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
   }
 }
 
-// ---- cooperative single-launch GroupNorm (round 4): kCoopNS blocks of 256 threads per (frame, group), each owning a
-// run of about hw / kCoopNS rows that it keeps in registers.  The one-block-per-group form above streams the whole
-// group slice through one CU (7-12 us per launch at UNet levels 2-3, a 108 / 432-pixel frame); here every block reads
-// an eighth of it, publishes its fp64 partial sums and meets the group's other blocks at an arrival counter, then
-// folds the kCoopNS partials in slot order (every block the same bits: deterministic) and normalises its rows.
-// Hand-off (MI355X_MICROARCH.md, the first row of the hand-off table): one lane stores the block's partials with sc1
-// (relaxed agent-scope atomic stores), waits for them (vmcnt(0)), then adds to the group's agent-scope counter; the
-// readers poll the counter with sc1 loads and read the slots with sc1 loads behind a workgroup barrier.  The last block
-// to leave resets the counters (the next launch is ordered behind this one by the kernel boundary).  All kCoopNS blocks
-// of a group must be resident together: the host takes this form only for grids of at most kCoopMaxBlocks blocks
-// (<= 4 blocks of 256 threads per CU), and every spin is bounded (g_coop_timeouts counts a bound reached; tests read
-// it through dc_gn_coop_timeouts).  Opt-in, DC_GN_COOP=1 (gn_coop_fits).
-constexpr int kCoopNS = 8;
-constexpr int kCoopKMax = 4;            // rows per thread held in registers
-constexpr int kCoopMaxBlocks = 1024;
-constexpr int kCoopSlots = kCoopMaxBlocks / kCoopNS;   // (frame, group) pairs per launch
-__device__ double g_coop_part[kCoopMaxBlocks * 2];
-__device__ unsigned g_coop_arrive[kCoopSlots];
-__device__ unsigned g_coop_depart[kCoopSlots];
-__device__ unsigned g_coop_timeouts;
-
-// publish (a, b), wait for the group's kCoopNS partials, return their slot-order sums in every thread
-__device__ __forceinline__ void gn_coop_exchange(int L, int sidx, double a, double b, double* red, double& ta,
-                                                 double& tb) {
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&g_coop_part[(L * kCoopNS + sidx) * 2], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&g_coop_part[(L * kCoopNS + sidx) * 2 + 1], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(&g_coop_arrive[L], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    while (__hip_atomic_load(&g_coop_arrive[L], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)kCoopNS) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {
-        __hip_atomic_fetch_add(&g_coop_timeouts, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    double sa = 0.0, sb = 0.0;
-#pragma unroll
-    for (int k = 0; k < kCoopNS; ++k) {
-      sa += __hip_atomic_load(&g_coop_part[(L * kCoopNS + k) * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sb += __hip_atomic_load(&g_coop_part[(L * kCoopNS + k) * 2 + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    red[0] = sa;
-    red[1] = sb;
-    // the last block out resets the group's counters (every block has passed its poll by then)
-    if (__hip_atomic_fetch_add(&g_coop_depart[L], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        (unsigned)kCoopNS - 1) {
-      __hip_atomic_store(&g_coop_arrive[L], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&g_coop_depart[L], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  ta = red[0];
-  tb = red[1];
-}
-
-// fixed-order fp64 reduction of (a, b) over a 256-thread block (result in thread 0's red[2..3] and returned to all)
-__device__ __forceinline__ void gn_coop_block_sum(float a, float b, double* red, double& ta, double& tb) {
-  double da = a, db = b;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    da += __shfl_xor(da, o, 64);
-    db += __shfl_xor(db, o, 64);
-  }
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    red[4 + w] = da;
-    red[8 + w] = db;
-  }
-  __syncthreads();
-  ta = (red[4] + red[5]) + (red[6] + red[7]);
-  tb = (red[8] + red[9]) + (red[10] + red[11]);
-}
-
-template <int VEC>
-__global__ __launch_bounds__(256) void gn_coop_fwd_kernel(GNShape s, int vpr, int RP, float eps, const float* gamma,
-                                                          const float* beta, int silu, bf16* y, int ldy, float* stats) {
-  __shared__ double red[12];
-  const int L = blockIdx.x / kCoopNS, sidx = blockIdx.x - L * kCoopNS;
-  const int n = L / s.groups, g = L % s.groups;
-  const int v = threadIdx.x % vpr, r0 = threadIdx.x / vpr;
-  const bool act = r0 < RP;
-  const int rows = (s.hw + kCoopNS - 1) / kCoopNS;
-  const int rbeg = sidx * rows, rend = min(s.hw, rbeg + rows);
-  const int ch = g * s.cpg + v * VEC;
-  long ld;
-  const bf16* src = gn_group_src(s, n, ch, ld);
-  bfvec<VEC> raw[kCoopKMax];
-#pragma unroll
-  for (int k = 0; k < kCoopKMax; ++k) {
-    const int row = rbeg + r0 + k * RP;
-    raw[k] = (act && row < rend) ? *reinterpret_cast<const bfvec<VEC>*>(src + row * ld) : bfvec<VEC>{};
-  }
-  float s1 = 0.0f, s2 = 0.0f;
-#pragma unroll
-  for (int k = 0; k < kCoopKMax; ++k)
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      const float f = (float)raw[k][i];
-      s1 += f;
-      s2 += f * f;
-    }
-  double pa, pb, ta, tb;
-  gn_coop_block_sum(s1, s2, red, pa, pb);
-  gn_coop_exchange(L, sidx, pa, pb, red, ta, tb);
-  const double cnt = (double)s.hw * s.cpg;
-  const double mu_d = ta / cnt;
-  double var = tb / cnt - mu_d * mu_d;
-  if (var < 0.0) var = 0.0;
-  const float mu = (float)mu_d, rs = (float)(1.0 / sqrt(var + (double)eps));
-  if (sidx == 0 && threadIdx.x == 0) {
-    stats[((long)n * s.groups + g) * 2] = mu;
-    stats[((long)n * s.groups + g) * 2 + 1] = rs;
-  }
-  if (!act) return;
-  float ga[VEC], be[VEC];
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    ga[i] = gamma[ch + i];
-    be[i] = beta[ch + i];
-  }
-  bf16* dst = y + (long)n * s.hw * ldy + ch;
-#pragma unroll
-  for (int k = 0; k < kCoopKMax; ++k) {
-    const int row = rbeg + r0 + k * RP;
-    if (row >= rend) continue;
-    bfvec<VEC> o;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      float t = ((float)raw[k][i] - mu) * rs * ga[i] + be[i];
-      if (silu) t = silu_f((float)(bf16)t);
-      o[i] = (bf16)t;
-    }
-    *reinterpret_cast<bfvec<VEC>*>(dst + (long)row * ldy) = o;
-  }
-}
-
-template <int VEC>
-__global__ __launch_bounds__(256) void gn_coop_bwd_kernel(GNShape s, int vpr, int RP, const float* stats,
-                                                          const float* gamma, const float* beta, int silu,
-                                                          const bf16* dy, int lddy, bf16* dx, int lddx,
-                                                          const bf16* add1, int ldadd1, const bf16* add2, int ldadd2) {
-  __shared__ double red[12];
-  const int L = blockIdx.x / kCoopNS, sidx = blockIdx.x - L * kCoopNS;
-  const int n = L / s.groups, g = L % s.groups;
-  const int v = threadIdx.x % vpr, r0 = threadIdx.x / vpr;
-  const bool act = r0 < RP;
-  const int rows = (s.hw + kCoopNS - 1) / kCoopNS;
-  const int rbeg = sidx * rows, rend = min(s.hw, rbeg + rows);
-  const int ch = g * s.cpg + v * VEC;
-  long ld;
-  const bf16* src = gn_group_src(s, n, ch, ld);
-  const long pix0 = (long)n * s.hw;
-  bfvec<VEC> rx[kCoopKMax], rd[kCoopKMax], e1[kCoopKMax], e2[kCoopKMax];
-#pragma unroll
-  for (int k = 0; k < kCoopKMax; ++k) {
-    const int row = rbeg + r0 + k * RP;
-    const bool ok = act && row < rend;
-    rx[k] = ok ? *reinterpret_cast<const bfvec<VEC>*>(src + row * ld) : bfvec<VEC>{};
-    rd[k] = ok ? *reinterpret_cast<const bfvec<VEC>*>(dy + (pix0 + row) * lddy + ch) : bfvec<VEC>{};
-    if (add1 && ok) e1[k] = *reinterpret_cast<const bfvec<VEC>*>(add1 + (pix0 + row) * ldadd1 + ch);
-    if (add2 && ok) e2[k] = *reinterpret_cast<const bfvec<VEC>*>(add2 + (pix0 + row) * ldadd2 + ch);
-  }
-  const float mu = stats[((long)n * s.groups + g) * 2], rs = stats[((long)n * s.groups + g) * 2 + 1];
-  float ga[VEC], be[VEC];
-#pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    ga[i] = act ? gamma[ch + i] : 0.0f;
-    be[i] = act ? beta[ch + i] : 0.0f;
-  }
-  // dy' = dy * silu'(y) rounded as bf16 autograd does (gn_group_bwd_kernel); returns g * dy' and xhat
-  auto elem = [&](float f, float d, int i, float& xh) {
-    xh = (f - mu) * rs;
-    float dd = d;
-    if (silu) {
-      const float yv = (float)(bf16)(xh * ga[i] + be[i]);
-      dd = (float)(bf16)(dd * silu_grad(yv));
-    }
-    return dd * ga[i];
-  };
-  float sa = 0.0f, sb = 0.0f;
-#pragma unroll
-  for (int k = 0; k < kCoopKMax; ++k) {
-    if (!act || rbeg + r0 + k * RP >= rend) continue;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      float xh;
-      const float gd = elem((float)rx[k][i], (float)rd[k][i], i, xh);
-      sa += gd;
-      sb += gd * xh;
-    }
-  }
-  double pa, pb, ta, tb;
-  gn_coop_block_sum(sa, sb, red, pa, pb);
-  gn_coop_exchange(L, sidx, pa, pb, red, ta, tb);
-  const double cnt = (double)s.hw * s.cpg;
-  const float ma = (float)(ta / cnt), mb = (float)(tb / cnt);
-  if (!act) return;
-  bf16* dst = dx + pix0 * lddx + ch;
-#pragma unroll
-  for (int k = 0; k < kCoopKMax; ++k) {
-    const int row = rbeg + r0 + k * RP;
-    if (row >= rend) continue;
-    float out[VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      float xh;
-      const float gd = elem((float)rx[k][i], (float)rd[k][i], i, xh);
-      out[i] = rs * (gd - ma - xh * mb);
-    }
-    if (add1) {
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) out[i] = (float)(bf16)out[i] + (float)e1[k][i];
-    }
-    if (add2) {
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) out[i] = (float)(bf16)out[i] + (float)e2[k][i];
-    }
-    bfvec<VEC> o;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) o[i] = (bf16)out[i];
-    *reinterpret_cast<bfvec<VEC>*>(dst + (long)row * lddx) = o;
-  }
-}
-
-// the cooperative form for a shape whose single-launch vector width is vec: every row of a block's run in registers
-// (vpr vectors per row, kCoopKMax rows per thread) and the grid within kCoopMaxBlocks.  Opt-in (DC_GN_COOP=1): at C2
-// it measured slower than the one-block-per-group kernels (1.5541 / 1.5524 vs 1.5610 / 1.5601 fps alternating on one
-// box, profiles/r04j): the counter fan-in costs more than the eighth of the slice each block saves.
-bool gn_coop_fits(const GNShape& s, int vec, int& vpr, int& RP) {
-  const char* e = getenv("DC_GN_COOP");
-  if (!e || atoi(e) == 0) return false;
-  if ((long)s.nb * s.groups * kCoopNS > kCoopMaxBlocks) return false;
-  vpr = s.cpg / vec;
-  if (vpr > 256) return false;
-  RP = 256 / vpr;
-  const int rows = (s.hw + kCoopNS - 1) / kCoopNS;
-  return rows <= RP * kCoopKMax;
-}
-
 bool gn_make_shape(GNShape& s, const void* x, int ldx, const void* x2, int ldx2, int c1, int nb, int hw, int c,
                    int groups) {
   if (!x || nb <= 0 || hw <= 0 || c <= 0 || groups <= 0 || groups > 64) return false;
@@ -991,21 +750,6 @@ extern "C" int dc_groupnorm_fwd(const void* x, int ldx, const void* x2, int ldx2
   if (ldy % 8) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   if (const int vec = gn_group_vec(s, 1, kGroupCapFwd, {s.x, s.x2, y})) {
-    int cvpr, cRP;
-    if (gn_coop_fits(s, vec, cvpr, cRP)) {
-      const dim3 cgrid(nb * groups * kCoopNS);
-      if (vec == 8)
-        hipLaunchKernelGGL(gn_coop_fwd_kernel<8>, cgrid, dim3(256), 0, st, s, cvpr, cRP, eps, gamma, beta, silu, (bf16*)y,
-                           ldy, stats);
-      else if (vec == 4)
-        hipLaunchKernelGGL(gn_coop_fwd_kernel<4>, cgrid, dim3(256), 0, st, s, cvpr, cRP, eps, gamma, beta, silu, (bf16*)y,
-                           ldy, stats);
-      else
-        hipLaunchKernelGGL(gn_coop_fwd_kernel<2>, cgrid, dim3(256), 0, st, s, cvpr, cRP, eps, gamma, beta, silu, (bf16*)y,
-                           ldy, stats);
-      DC_CHECK_LAUNCH();
-      return DC_OK;
-    }
     const int vpr = s.cpg / vec, RP = kGroupThreads / vpr;
     const dim3 grid(nb * groups), blk(kGroupThreads);
     const size_t lds = kGroupRed + (size_t)hw * s.cpg * 2;
@@ -1041,22 +785,6 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   if (lddy % 8 || lddx % 8 || (add1 && ldadd1 % 8) || (add2 && ldadd2 % 8)) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   if (const int vec = gn_group_vec(s, 2, kGroupCapBwd, {s.x, s.x2, dy, dx, add1 ? add1 : dx, add2 ? add2 : dx})) {
-    int cvpr, cRP;
-    if (gn_coop_fits(s, vec, cvpr, cRP)) {
-      const dim3 cgrid(nb * groups * kCoopNS);
-#define DC_GN_COOP_BWD(V)                                                                                       \
-  hipLaunchKernelGGL(gn_coop_bwd_kernel<V>, cgrid, dim3(256), 0, st, s, cvpr, cRP, stats, gamma, beta, silu,     \
-                     (const bf16*)dy, lddy, (bf16*)dx, lddx, (const bf16*)add1, ldadd1, (const bf16*)add2, ldadd2)
-      if (vec == 8)
-        DC_GN_COOP_BWD(8);
-      else if (vec == 4)
-        DC_GN_COOP_BWD(4);
-      else
-        DC_GN_COOP_BWD(2);
-#undef DC_GN_COOP_BWD
-      DC_CHECK_LAUNCH();
-      return DC_OK;
-    }
     const int vpr = s.cpg / vec, RP = kGroupThreads / vpr;
     const dim3 grid(nb * groups), blk(kGroupThreads);
     const size_t lds = kGroupRed + 2 * (size_t)hw * s.cpg * 2;
@@ -1097,13 +825,6 @@ extern "C" int dc_gn_fuse_pays(int hw, int c, int groups, int backward) {
   alignas(16) static const bf16 dummy[8] = {};
   if (!gn_make_shape(s, dummy, c, nullptr, 0, 0, 1, hw, c, groups)) return 0;
   return gn_group_vec(s, backward ? 2 : 1, backward ? kGroupCapBwd : kGroupCapFwd, {dummy}) ? 0 : 1;
-}
-
-// bound-reached count of the cooperative GroupNorm's spins since load (tests: must stay 0)
-extern "C" int dc_gn_coop_timeouts(void) {
-  unsigned v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_coop_timeouts), sizeof v, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  return (int)v;
 }
 
 extern "C" long long dc_gn_acc_bytes(int nb, int groups) {

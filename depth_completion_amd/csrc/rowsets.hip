@@ -192,3 +192,14 @@ extern "C" int dc_mask_rows(const unsigned char* mask, long long total, const in
   DC_CHECK_LAUNCH();
   return DC_OK;
 }
+
+// rows[count[0] .. pad_to) = the last listed pixel: the padding of dc_mask_rows(..., pad_to, ...) as its own launch,
+// for hosts that list the rows before they know pad_to (the padded size waits for count[0] on the host)
+extern "C" int dc_pad_rows(int* rows, const int* count, int pad_to, void* stream) {
+  if (!rows || !count || pad_to < 0) return DC_ERR_ARG;
+  if (pad_to == 0) return DC_OK;
+  hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)min((pad_to + 255) / 256, 1024)), dim3(256), 0,
+                     (hipStream_t)stream, rows, count, pad_to);
+  DC_CHECK_LAUNCH();
+  return DC_OK;
+}

@@ -663,7 +663,11 @@ class UNetPlan {
   std::map<const void*, std::unique_ptr<dc_gn_fuse>> gn_fuse_;        // built at the first call
   std::vector<std::unique_ptr<dc_gn_fuse>> gn_bwd_;                     // backward fuses (fixed at build)
 
-  long long* gn_acc() { return gn_arena_ + (size_t)(gn_next_++) * gn_words_; }
+  long long* gn_acc() {   // a GroupNorm site the arena was not sized for: fail, never hand out past its end
+    if ((size_t)(gn_next_ + 1) * gn_words_ * 8 > gn_arena_bytes_)
+      throw DcError(kErrArg, "GroupNorm accumulator arena exhausted (" + std::to_string(gn_next_) + " slots)");
+    return gn_arena_ + (size_t)(gn_next_++) * gn_words_;
+  }
   bool gn_pays(int hw, int c, bool backward) { return fuse_gn_ && dc_gn_fuse_pays(hw, c, 32, backward ? 1 : 0); }
   long long* gn_consumer(RB x, int c, int hw, RB x2 = RB(), int c1 = 0) {
     if (!gn_pays(hw, c, false)) return nullptr;
@@ -1689,12 +1693,20 @@ int guarded(dc_session* s, void* user_stream, F&& f) {
   try {
     HIPK(hipSetDevice(s->device));
     if (!s->loaded) throw DcError(kErrArg, "no weights loaded (dc_load_weights)");
-    // order the session stream after the caller's work, and the caller's stream after ours -- also when f()
-    // throws after queueing work that reads the caller's buffers (the guard's destructor joins the streams
-    // and destroys the event on every exit path)
+    // order the session stream after the caller's work, and the caller's stream after ours.  On success the join's
+    // statuses are checked (join() throws on a failed record / wait); when f() or the join throws after queueing
+    // work that reads the caller's buffers, the destructor still joins the streams, best effort, and destroys the
+    // event on every exit path
     struct StreamJoin {
       hipEvent_t e = nullptr;
       hipStream_t sess, user;
+      void join() {
+        HIPK(hipEventRecord(e, sess));
+        HIPK(hipStreamWaitEvent(user, e, 0));
+        const hipError_t d = hipEventDestroy(e);
+        e = nullptr;
+        if (d != hipSuccess) throw DcError(kErrLaunch, std::string("hipEventDestroy: ") + hipGetErrorString(d));
+      }
       ~StreamJoin() {
         if (!e) return;
         (void)hipEventRecord(e, sess);
@@ -1706,6 +1718,7 @@ int guarded(dc_session* s, void* user_stream, F&& f) {
     HIPK(hipEventRecord(join.e, (hipStream_t)user_stream));
     HIPK(hipStreamWaitEvent(s->stream, join.e, 0));
     f();
+    join.join();
     s->err.clear();
     return kOK;
   } catch (const DcError& e) {

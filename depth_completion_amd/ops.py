@@ -258,6 +258,10 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
         # a GroupNorm-fused call runs skinny / resident / wide choices as the library heuristic (those kernels have
         # no fused-statistics epilogue): never offer them, so the table only holds configurations that were timed
         cands = [c for c in cands if not SKINNY_FIRST <= c[0] <= WIDE_LAST]
+    if d.ln:
+        # a LayerNorm-folded linear (dc_conv_gemm's ln branch) runs on the im2col tiles only: any other choice would be
+        # replaced by the library heuristic, so the table would store an id whose timing was the heuristic's
+        cands = [c for c in cands if c == (0, 0) or 1 <= c[0] <= IM2COL_LAST and not HALO_FIRST <= c[0] <= HALO_LAST]
     if getattr(ctx, "tune_only", None):   # tools/tune_gemm.py --try: the committed choice against these algos only
         cur = ctx.tune_only[1].get(conv_key(d))
         cands = ([cur] if cur else []) + [c for c in cands if c[0] in ctx.tune_only[0]]

@@ -313,10 +313,36 @@ class MarigoldDepthCompletionPipeline:
         up, dp = st["unet"], st["dec"]
         P = n * h * w
 
+        # The call reads the device back once (the guide counts and the row-set sizes, below), and its inputs reach
+        # the device without a pageable host copy (each would wait for all queued work, the previous call's steps
+        # included, with the GPU idle behind it): the read is queued first and lands while the encoder runs.
+        HWs = H * W
+        io = self._io(st, n, H, W)
+        idx, gval, cnt, params, gmap = io["idx"], io["gval"], io["cnt"], io["params"], io["gmap"]
+
+        # ---- sparse guides (marigold_dc.py:706-756)
+        lohi = None
+        if norm == "percentile":
+            # torch.quantile over the masked values (setup, once per call; marigold_dc.py:714-726)
+            q = torch.tensor(percentile, dtype=torch.float32)
+            sp_cpu = sparses.cpu()
+            lohi = torch.stack([torch.quantile(s[s > 0], q) for s in sp_cpu]).to(dev).contiguous()
+        _lib.call("dc_sparse_setup", sparses.data_ptr(), n, H, W, _NORM[norm], float(min_depth), float(max_depth),
+                  ops.P(lohi), _PROJ[projection], int(inv), _INTERP[interp_mode], idx.data_ptr(), gval.data_ptr(),
+                  cnt.data_ptr(), params.data_ptr(), ctx.stream)
+        # ---- sparse-aware decode (guided steps with the point losses read the decode only at the taps): the row
+        # sets' masks, sizes and sorted lists; only their padding waits for the sizes on the host
+        want_rows = guided and not full_loss and self.vae_kind == "light" and self.sparse_decode
+        if want_rows:
+            self._row_sets(st, idx, cnt, params, n, PH, PW, RH, RW, H, W)
+        io["counts_host"].copy_(io["counts"], non_blocking=True)
+        io["counts_ready"].record(torch.cuda.current_stream(dev))
+
         # ---- initial latents (marigold_dc.py:661, 677-704)
-        gen = torch.Generator().manual_seed(seed)
-        noise = torch.randn((1, 4, h, w), generator=gen, dtype=BF16) if init_noise is None else init_noise
-        noise = noise.to(dev, BF16).contiguous()
+        if init_noise is None:   # the same draw every call of a seed: kept on the device
+            noise = self._noise(seed, h, w)
+        else:
+            noise = init_noise.to(dev, BF16).contiguous()
         # one draw for every frame, or one per frame (the per-seed draws of ensemble())
         if noise.ndim != 4 or tuple(noise.shape[1:]) != (4, h, w) or noise.shape[0] not in (1, n):
             raise ValueError(f"init_noise must be [1, 4, {h}, {w}] or [{n}, 4, {h}, {w}], got {tuple(noise.shape)}")
@@ -335,29 +361,9 @@ class MarigoldDepthCompletionPipeline:
         self.vae.encode(ctx, img8, n, PH, PW, ops.Slice(up.x8, 0))
         del img8
 
-        # ---- sparse guides (marigold_dc.py:706-756)
-        HWs = H * W
-        idx = torch.empty(n, HWs, dtype=torch.int32, device=dev)
-        gval = torch.empty(n, HWs, dtype=torch.float32, device=dev)
-        cnt = torch.empty(n, dtype=torch.int32, device=dev)
-        params = torch.empty(n, 8, dtype=torch.float32, device=dev)
-        lohi = None
-        if norm == "percentile":
-            # torch.quantile over the masked values (setup, once per call; marigold_dc.py:714-726)
-            q = torch.tensor(percentile, dtype=torch.float32)
-            sp_cpu = sparses.cpu()
-            lohi = torch.stack([torch.quantile(s[s > 0], q) for s in sp_cpu]).to(dev).contiguous()
-        _lib.call("dc_sparse_setup", sparses.data_ptr(), n, H, W, _NORM[norm], float(min_depth), float(max_depth),
-                  ops.P(lohi), _PROJ[projection], int(inv), _INTERP[interp_mode], idx.data_ptr(), gval.data_ptr(),
-                  cnt.data_ptr(), params.data_ptr(), ctx.stream)
-        cnt_host = cnt.cpu()
-        if (cnt_host == 0).any():
-            raise ValueError("No valid values found in mask for some positions. "
-                             "Ensure that mask has at least one True value along the specified dimensions.")
         # full-image losses: dense guide map + the caller's uint8 image (edge term's gray gradients)
-        gmap = torch.empty(n, HWs, dtype=torch.float32, device=dev)
-        img_u8 = imgs.contiguous()
         if full_loss and (guided or fit_affine):
+            io["img"].copy_(imgs.reshape(io["img"].shape))
             _lib.call("dc_guide_map", idx.data_ptr(), gval.data_ptr(), cnt.data_ptr(), n, H, W, gmap.data_ptr(),
                       ctx.stream)
             nws = _lib.load().dc_dense_loss_ws_bytes(n, H, W)
@@ -367,24 +373,27 @@ class MarigoldDepthCompletionPipeline:
                 st["cf_stats"] = torch.zeros(n, 8, dtype=torch.float32, device=dev)
                 st["cf_grad"] = torch.zeros(n, 2, dtype=torch.float32, device=dev)
 
-        # ---- sparse-aware decode (guided steps with the point losses read the decode only at the taps)
-        row_counts = ()
-        rows = None
-        if guided and not full_loss and self.vae_kind == "light" and self.sparse_decode:
-            rows, row_counts = self._decode_rows(st, idx, cnt, params, n, PH, PW, RH, RW, H, W)
-        dp.set_rows(rows)
-        st["row_sets"] = rows
-
-        # ---- per-call tables
-        ts = self.scheduler.timesteps(steps)
-        coef = self.scheduler.coef(steps).to(dev)
-        adam = adam_table(steps, lr_latent, lr_scaling, opt_code).to(dev)
+        # ---- per-call tables (device copies kept per (steps, learning rates, optimiser))
+        ts, coef, adam = self._step_tables(steps, lr_latent, lr_scaling, opt_code)
         self.unet.build_temb_tables(ctx, ts)
         for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"], st["daff"]):
             ops.memset(ctx, t)
-        st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))
+        st["affine"].copy_(io["affine0"])
         ops.memset(ctx, ctx.step)
         cf = bool(closed_form)
+        img_u8 = io["img"]
+
+        # ---- the call's device read: empty masks raise (utils.py:132-136), the row sets get padded
+        io["counts_ready"].synchronize()
+        if (io["counts_host"][:n] == 0).any():
+            raise ValueError("No valid values found in mask for some positions. "
+                             "Ensure that mask has at least one True value along the specified dimensions.")
+        row_counts = ()
+        rows = None
+        if want_rows:
+            rows, row_counts = self._pad_rows(st, io["counts_host"][n:].tolist(), n * PH * PW)
+        dp.set_rows(rows)
+        st["row_sets"] = rows
         self._call_state = dict(idx=idx, gval=gval, cnt=cnt, params=params, coef=coef, adam=adam, gmap=gmap,
                                 img=img_u8, H=H, W=W, RH=RH, RW=RW, PH=PH, PW=PW, n=n, h=h, w=w, cf=cf,
                                 opt=opt_code, kld=kld_code, kld_weight=float(kld_weight),
@@ -397,9 +406,9 @@ class MarigoldDepthCompletionPipeline:
             gkey = (guided, guided and cf, opt_code, kld_code, float(kld_weight), steps, H, W, RH, RW, lr_latent,
                     lr_scaling, loss_flags if full_loss else 0, row_counts)
             if g is None or st["graph_key"] != gkey:
-                # (re)capture against this call's tables: they become the graph's tables before the warm-up and
-                # the capture read them through _tables(), and the previous graph is dropped first, as it binds
-                # the tables being replaced
+                # (re)capture: the graph binds this call's tables -- the plan's persistent guide buffers for (n, H, W)
+                # and the kept (steps, lr, optimiser) tables, which later calls with the same key rewrite in place
+                # or reuse (gkey covers every one of them); the previous graph is dropped first
                 st["graph"], st["graph_key"] = None, None
                 st["graph_tables"] = (coef, adam, idx, gval, cnt, params, gmap, img_u8)
                 g = torch.cuda.CUDAGraph()
@@ -411,15 +420,10 @@ class MarigoldDepthCompletionPipeline:
                 torch.cuda.current_stream(dev).wait_stream(s)
                 torch.cuda.synchronize(dev)
                 # undo the warm-up step's state change
-                self._reset_state(st, n, noise, prev, beta)
+                self._reset_state(st, io, n, noise, prev, beta)
                 with torch.cuda.graph(g):
                     step_fn(st)
                 st["graph"], st["graph_key"] = g, gkey
-            else:
-                # replay reads the captured table addresses: refresh their contents in place
-                old = st["graph_tables"]
-                for dst, src in zip(old, (coef, adam, idx, gval, cnt, params, gmap, img_u8)):
-                    dst.copy_(src)
             for _ in range(steps):
                 g.replay()
         else:
@@ -513,35 +517,89 @@ class MarigoldDepthCompletionPipeline:
     _ROW_PAD = 4096
     _ROW_KEYS = ("out", "c3", "c2", "c1", "up", "dhi")
 
-    def _decode_rows(self, st, idx, cnt, params, n, PH, PW, RH, RW, H, W):
-        """Row lists of the full-resolution decoder level for the point losses; (None, ()) when the largest
-        set covers most of the map (dense is then as fast)."""
+    def _row_sets(self, st, idx, cnt, params, n, PH, PW, RH, RW, H, W):
+        """Row sets S0..S5 of the full-resolution decoder level for the point losses: masks (tap mask, then 3x3
+        dilations), their sizes into the call's device counts (read back with the guide counts) and their sorted row
+        lists; _pad_rows pads the lists once the sizes are on the host."""
         ctx = self.ctx
         total = n * PH * PW
+        K = len(self._ROW_KEYS)
         if st.get("row_masks") is None or st["row_masks"].shape[1] != total:
-            st["row_masks"] = torch.empty(len(self._ROW_KEYS), total, dtype=torch.uint8, device=self.device)
-            st["row_lists"] = torch.empty(len(self._ROW_KEYS), total, dtype=torch.int32, device=self.device)
-            st["row_ws"] = torch.empty(-(-_lib.load().dc_mask_rows_ws_bytes(total) // 4), dtype=torch.int32,
-                                       device=self.device)
-            st["row_cnt"] = torch.zeros(len(self._ROW_KEYS), dtype=torch.int32, device=self.device)
-        masks, lists, ws, cntd = st["row_masks"], st["row_lists"], st["row_ws"], st["row_cnt"]
+            st["row_masks"] = torch.empty(K, total, dtype=torch.uint8, device=self.device)
+            st["row_lists"] = torch.empty(K, total, dtype=torch.int32, device=self.device)
+            nws = -(-_lib.load().dc_mask_rows_ws_bytes(total) // 4)
+            st["row_ws"] = torch.empty(K, nws, dtype=torch.int32, device=self.device)   # one scan per set
+        masks, lists, ws = st["row_masks"], st["row_lists"], st["row_ws"]
+        cntd = self._io(st, n, H, W)["counts"][n:]
         _lib.call("dc_tap_mask", idx.data_ptr(), cnt.data_ptr(), params.data_ptr(), n, PH, PW, RH, RW, H, W,
                   masks[0].data_ptr(), ctx.stream)
-        for k in range(1, len(self._ROW_KEYS)):
+        for k in range(1, K):
             _lib.call("dc_dilate_mask", masks[k - 1].data_ptr(), n, PH, PW, masks[k].data_ptr(), ctx.stream)
-        rows, counts = {}, []
-        for k, key in enumerate(self._ROW_KEYS):
-            _lib.call("dc_mask_count", masks[k].data_ptr(), total, ws.data_ptr(), cntd[k:].data_ptr(), ctx.stream)
-            c = int(cntd[k].item())
-            if k == len(self._ROW_KEYS) - 1 and c > 0.6 * total:
-                return None, ()
+        for k in range(K):
+            _lib.call("dc_mask_count", masks[k].data_ptr(), total, ws[k].data_ptr(), cntd[k:].data_ptr(), ctx.stream)
+            _lib.call("dc_mask_rows", masks[k].data_ptr(), total, ws[k].data_ptr(), cntd[k:].data_ptr(), 0,
+                      lists[k].data_ptr(), ctx.stream)
+
+    def _pad_rows(self, st, counts, total):
+        """Pad the row lists of _row_sets (host sizes `counts`) up to their buckets: ({key: (list, rows)}, the
+        padded sizes), or (None, ()) when the largest set covers most of the map (dense is then as fast)."""
+        if counts[-1] > 0.6 * total:
+            return None, ()
+        lists, cntd = st["row_lists"], self._last_io["counts"][self._last_io["n"]:]
+        rows, padded = {}, []
+        for k, (key, c) in enumerate(zip(self._ROW_KEYS, counts)):
             gran = max(self._ROW_PAD, (1 << max(c - 1, 1).bit_length()) // 4)
             pad = min(total, -(-max(c, 1) // gran) * gran)
-            _lib.call("dc_mask_rows", masks[k].data_ptr(), total, ws.data_ptr(), cntd[k:].data_ptr(), pad,
-                      lists[k].data_ptr(), ctx.stream)
+            _lib.call("dc_pad_rows", lists[k].data_ptr(), cntd[k:].data_ptr(), pad, self.ctx.stream)
             rows[key] = (lists[k], pad)
-            counts.append(pad)
-        return rows, tuple(counts)
+            padded.append(pad)
+        return rows, tuple(padded)
+
+    def _io(self, st, n, H, W):
+        """The call's guide buffers for (n, H, W), kept with the plan: a captured step graph binds their addresses,
+        and every call rewrites them in place (idx / gval / cnt / params: dc_sparse_setup; gmap: dc_guide_map; img:
+        the caller's uint8 image for the edge term).  counts = (guide counts [n], row-set sizes [6]) on the device,
+        read back into the pinned counts_host once per call."""
+        key = ("io", n, H, W)
+        io = st.get(key)
+        if io is None:
+            dev = self.device
+            io = dict(n=n,
+                      idx=torch.empty(n, H * W, dtype=torch.int32, device=dev),
+                      gval=torch.empty(n, H * W, dtype=torch.float32, device=dev),
+                      params=torch.empty(n, 8, dtype=torch.float32, device=dev),
+                      gmap=torch.empty(n, H * W, dtype=torch.float32, device=dev),
+                      img=torch.empty(n, 3, H, W, dtype=torch.uint8, device=dev),
+                      counts=torch.zeros(n + len(self._ROW_KEYS), dtype=torch.int32, device=dev),
+                      counts_host=torch.zeros(n + len(self._ROW_KEYS), dtype=torch.int32, pin_memory=True),
+                      counts_ready=torch.cuda.Event(),
+                      affine0=torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32).to(dev))
+            io["cnt"] = io["counts"][:n]
+            st[key] = io
+        self._last_io = io
+        return io
+
+    def _noise(self, seed, h, w):
+        """The initial noise of marigold_dc.py:677-684 for `seed` (CPU torch.Generator, [1, 4, h, w] bf16), drawn once
+        and kept on the device."""
+        key = (int(seed), h, w)
+        cache = self.__dict__.setdefault("_noise_cache", {})
+        if key not in cache:
+            if len(cache) > 64:
+                cache.clear()
+            gen = torch.Generator().manual_seed(int(seed))
+            cache[key] = torch.randn((1, 4, h, w), generator=gen, dtype=BF16).to(self.device).contiguous()
+        return cache[key]
+
+    def _step_tables(self, steps, lr_latent, lr_scaling, opt_code):
+        """(timesteps (host), DDIM coefficients, optimiser scalars (device)) for a step count, learning rates and
+        optimiser; kept, so that repeated calls neither recompute them nor copy them to the device."""
+        key = (int(steps), float(lr_latent), float(lr_scaling), int(opt_code), repr(sorted(self.scheduler.config.items())))
+        cache = self.__dict__.setdefault("_step_table_cache", {})
+        if key not in cache:
+            ts, coef, adam = self.scheduler._tables(steps, (lr_latent, lr_scaling), opt_code)
+            cache[key] = (ts, coef.to(self.device), adam.to(self.device))
+        return cache[key]
 
     def _vae_input(self, lat_ptr, P, dp):
         """decode_prediction's VAE input from the latents at lat_ptr ([P][8] rows, 4 channels): TAESD's
@@ -553,20 +611,16 @@ class MarigoldDepthCompletionPipeline:
                       self.ctx.stream)
 
     def _tables(self, st):
-        cs = self._call_state
-        if self.use_graph and st.get("graph_tables") is not None:
-            coef, adam, idx, gval, cnt, params, gmap, img = st["graph_tables"]
-            return dict(cs, coef=coef, adam=adam, idx=idx, gval=gval, cnt=cnt, params=params, gmap=gmap, img=img)
-        return cs
+        return self._call_state
 
-    def _reset_state(self, st, n, noise, prev, beta):
+    def _reset_state(self, st, io, n, noise, prev, beta):
         ctx = self.ctx
         up = st["unet"]
         _lib.call("dc_latent_init", noise.data_ptr(), noise.shape[0], ops.P(prev), float(beta), n, up.h * up.w,
                   up.x8.data_ptr(), ctx.stream)
         for t in (st["m_lat"], st["v_lat"], st["m_aff"], st["v_aff"]):
             ops.memset(ctx, t)
-        st["affine"].copy_(torch.tensor([[1.0, 0.0]] * n, dtype=torch.float32))
+        st["affine"].copy_(io["affine0"])
         ops.memset(ctx, ctx.step)
 
     def _ddim_step(self, st):

@@ -123,6 +123,7 @@ class UNetHIP:
         self.norm_out = Norm(sd["conv_norm_out.weight"], sd["conv_norm_out.bias"], dev, 1e-5)
         # conv_out 320->4: forward output padded to ld 8; input-gradient reads dv [P][8] (4..7 zero)
         self.conv_out = Conv(sd["conv_out.weight"], sd["conv_out.bias"], dev, dgrad_cout_pad=8)
+        self._temb_key: dict = {}   # step count -> the timesteps its temb tables were built for
 
     def resnets(self):
         for blk in self.down:
@@ -138,6 +139,11 @@ class UNetHIP:
         time_emb_proj(SiLU(emb)) to conv1's output (ResnetBlock2D).  Run on the device kernels.
         """
         S = timesteps.shape[0]
+        key = tuple(int(t) for t in timesteps.detach().cpu().tolist())
+        if self._temb_key.get(S) == key:   # the tables of these timesteps are already built (weights are fixed)
+            for r in self.resnets():
+                r.temb_table = r.temb_tables[S]
+            return
         c0 = self.cfg.block_out_channels[0]
         te = timestep_embedding(timesteps.cpu(), c0).to(BF16).to(self.device)
         d = self.cfg.time_embed_dim
@@ -155,6 +161,7 @@ class UNetHIP:
                 r.temb_tables[S] = torch.empty(S, r.cout, dtype=BF16, device=self.device)
             r.temb_table = r.temb_tables[S]
             ops.linear(ctx, semb, r.temb.wf, S, r.cout, r.temb_table, bias=r.temb.bias)
+        self._temb_key[S] = key
 
     def plan(self, ctx: Ctx, nb: int, h: int, w: int) -> "UNetPlan":
         return UNetPlan(self, ctx, nb, h, w)

@@ -34,11 +34,11 @@ const char* dc_build_id(void);
  */
 /* GroupNorm statistics fused into the epilogue of the conv / linear that produces the normalised tensor
  * (diffusers ResnetBlock2D norm1 / norm2, Transformer2DModel.norm, conv_norm_out: every GroupNorm input of the
- * UNet is a conv or linear output, and so is every GroupNorm output-gradient).  The sums go into exact
+ * UNet is a conv or linear output, and so is every GroupNorm output-gradient).  The sums go into fixed-point
  * accumulators of dc_gn_acc_bytes(nb, groups) bytes (zero-filled before the producers run): per (frame, group)
- * two quantities, each an integer of 8 32-bit limbs (LSB 2^-120) plus a non-finite count, to which every fp32
- * contribution is added with integer atomics -- the sums are exact, so they do not depend on tile order or
- * arrival order (bitwise reproducible).  dc_groupnorm_fwd_acc / dc_groupnorm_bwd_acc then normalise in one pass.
+ * two quantities, each an integer of 8 32-bit limbs (LSB 2^-120) plus a non-finite count, to which every block's
+ * fp32 partial (its tile folded in a fixed order) is added with integer atomics -- the sum of the partials is
+ * exact, so it does not depend on tile order or arrival order (bitwise reproducible); the partials are fp32.  dc_groupnorm_fwd_acc / dc_groupnorm_bwd_acc then normalise in one pass.
  *   mode 1 (forward): (sum y, sum y^2) of the stored bf16 outputs into t[0 .. nt-1] (one output may be both the
  *          direct input of one GroupNorm and the skip half (coff = c1) of an up-block concat);
  *   mode 2 (backward): the output is dL/d(GroupNorm(+SiLU) output); with the GroupNorm input x (x2: channels
@@ -161,10 +161,6 @@ int dc_groupnorm_bwd_acc(const void* x, int ldx, const void* x2, int ldx2, int c
                          const float* gamma, const float* stats, const long long* acc, const void* dyp, int lddy,
                          void* dx, int lddx, const void* add1, int ldadd1, const void* add2, int ldadd2,
                          void* stream);
-/* count of spin bounds reached by the cooperative single-launch GroupNorm since load (8 blocks per (frame, group)
- * meeting at an arrival counter; opt-in with DC_GN_COOP=1 for UNet level-2 / 3 slices at up to 4 frames; by default one
- * block per group): 0 unless the blocks of a group were not resident together (tests check it) */
-int dc_gn_coop_timeouts(void);
 int dc_layernorm_fwd(const void* x, int ldx, long long rows, int c, float eps, const float* gamma, const float* beta,
                      void* y, int ldy, float* stats, void* stream);
 /* gamma NULL: dy is already gamma * dL/dy (the input-gradient of a dc_ln_fuse folded weight) */
@@ -324,6 +320,9 @@ long long dc_mask_rows_ws_bytes(long long total);
 int dc_mask_count(const unsigned char* mask, long long total, int* ws, int* count, void* stream);
 int dc_mask_rows(const unsigned char* mask, long long total, const int* ws, const int* count, int pad_to, int* rows,
                  void* stream);
+/* rows[count[0] .. pad_to) = rows[count[0] - 1]: dc_mask_rows' padding as its own launch (rows listed with pad_to 0
+ * before the host knows the padded size) */
+int dc_pad_rows(int* rows, const int* count, int pad_to, void* stream);
 
 /* ---------------------------------------------------------------- AutoencoderKL (--vae original)
  * decode_prediction's vae.decode(z / scaling_factor) (marigold_dc.py:366 via diffusers) for the 4 latent

@@ -57,7 +57,7 @@ def group_stats(y, n, hw, c, groups=G):
 
 
 # conv variants: (algo, nsplit) -- im2col tiles plain / split-K / stream-K, and halo tiles plain / split
-VARIANTS = [(3, 1), (13, 2), (10, 1), (1, -1), (18, 1), (23, 1), (29, 2), (31, 1), (33, 3)]
+VARIANTS = [(3, 1), (13, 2), (10, 1), (1, -1), (18, 1), (23, 1), (29, 2), (31, 1), (33, 3), (62, 1), (63, 2), (64, 1)]
 
 
 @pytest.mark.parametrize("algo,nsplit", VARIANTS)
@@ -157,7 +157,8 @@ def test_fused_linear_frames_straddle(ctx, n, t, c, algo):
 
 
 @pytest.mark.parametrize("silu,two,algo,nsplit", [(True, False, 3, 1), (True, True, 13, 2), (False, False, 1, -1),
-                                                  (True, False, 31, 1), (True, True, 29, 2)])
+                                                  (True, False, 31, 1), (True, True, 29, 2), (True, False, 62, 1),
+                                                  (True, True, 63, 2), (False, False, 64, 1)])
 def test_fused_backward(ctx, silu, two, algo, nsplit):
     """Mode 2: the conv producing dL/d(GN(+SiLU) output) stores dy' and sums (gamma dy', gamma dy' xhat); the
     one-pass backward then matches torch autograd and the separate-pass kernels."""

@@ -194,15 +194,13 @@ def test_small_cin_and_splitk_linear(ctx):
 
 
 # ----------------------------------------------------------------------------- norms
-@pytest.fixture(params=["group", "group1", "2pass", "3pass"])
+@pytest.fixture(params=["group", "2pass", "3pass"])
 def gn_path(request, monkeypatch):
-    """GroupNorm launch form: a single launch wherever the slice fits the LDS (DC_GN_GROUP=-1; by default only
-    small slices take it) -- 8 cooperating blocks per (frame, group) where their rows fit the registers ("group"),
-    or one block per (frame, group) ("group1", DC_GN_COOP=0) --, stats + apply with the finalize folded into every
+    """GroupNorm launch form: a single launch, one block per (frame, group), wherever the slice fits the LDS
+    (DC_GN_GROUP=-1; by default only small slices take it), stats + apply with the finalize folded into every
     apply block (DC_GN_GROUP=0), or stats / finalize / apply (DC_GN_GROUP=0, DC_GN_FUSED=0)."""
-    monkeypatch.setenv("DC_GN_GROUP", "-1" if request.param.startswith("group") else "0")   # -1: no size cap
+    monkeypatch.setenv("DC_GN_GROUP", "-1" if request.param == "group" else "0")   # -1: no size cap
     monkeypatch.setenv("DC_GN_FUSED", "0" if request.param == "3pass" else "1")
-    monkeypatch.setenv("DC_GN_COOP", "0" if request.param == "group1" else "1")   # (cooperative form: opt-in)
     return request.param
 
 
@@ -301,46 +299,6 @@ def test_groupnorm_paths_agree(ctx, monkeypatch, n, h, w, c, two):
     assert rel(d3, d2) < 5e-3
 
 
-@pytest.mark.parametrize("n,h,w,c,two", [(1, 18, 24, 1280, False), (1, 18, 24, 1920, True), (1, 18, 24, 640, False),
-                                        (1, 9, 12, 2560, True), (1, 9, 12, 1280, False), (2, 18, 24, 960, True),
-                                        (4, 9, 12, 1280, False)])
-def test_groupnorm_coop(ctx, monkeypatch, n, h, w, c, two):
-    """The cooperative single-launch GroupNorm (8 blocks per (frame, group) exchanging fp64 partials through an
-    arrival counter) at the UNet level-2 / 3 shapes: against torch fp32, against the one-block-per-group kernel
-    (the same fp32 inputs folded in another order), bit-identical on repeat, and no spin bound ever reached."""
-    from depth_completion_amd import _lib, ops
-    x = (rnd(n, c, h, w, seed=47) * 1.5 + 0.4).to(torch.bfloat16).float().requires_grad_(True)
-    gamma = (1 + 0.1 * rnd(c, seed=48)).to(torch.bfloat16).float()
-    beta = (0.1 * rnd(c, seed=49)).to(torch.bfloat16).float()
-    ref = F.silu(F.group_norm(x, 32, gamma, beta, eps=1e-5))
-    gyf = rnd(n, c, h, w, seed=50)
-    ref.backward(gyf)
-    xs = nhwc(x.detach())
-    c1 = (c // 2) // 64 * 64 if two else 0
-    xa, xb = (xs[:, :c1].contiguous(), xs[:, c1:].contiguous()) if two else (xs, None)
-    kw = dict(x2=xb, c1=c1) if two else {}
-    gy, add = nhwc(gyf), nhwc(rnd(n, c, h, w, seed=51))
-    monkeypatch.setenv("DC_GN_GROUP", "-1")
-    t0 = _lib.load().dc_gn_coop_timeouts()
-    res = {}
-    for path in ("coop", "coop2", "one"):
-        monkeypatch.setenv("DC_GN_COOP", "0" if path == "one" else "1")
-        y = torch.empty_like(xs)
-        stats = torch.empty(n, 32, 2, device=dev)
-        dx = torch.empty_like(xs)
-        ops.groupnorm(ctx, xa, n, h * w, c, gamma, beta, 1e-5, True, y, stats, **kw)
-        ops.groupnorm_bwd(ctx, xa, n, h * w, c, gamma, beta, True, stats, gy, dx, add1=add, **kw)
-        torch.cuda.synchronize()
-        res[path] = (y, stats, dx)
-    assert _lib.load().dc_gn_coop_timeouts() == t0
-    (y1, s1, d1), (y2, s2, d2), (y3, s3, d3) = res["coop"], res["coop2"], res["one"]
-    assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(d1, d2)
-    assert rel(s1, s3) < 1e-5
-    assert rel(y1, y3) < 2e-3 and rel(d1, d3) < 5e-3
-    assert rel(nchw(y1, n, h, w), ref) < 1e-2
-    assert rel(nchw(d1, n, h, w), x.grad + nchw(add, n, h, w)) < 2e-2
-
-
 @pytest.mark.parametrize("c", [64, 320, 1280])
 def test_layernorm_fwd_bwd(ctx, c):
     from depth_completion_amd import ops
@@ -389,6 +347,9 @@ def test_linear_ln_fused(ctx, c, n, geglu, algo, nsplit):
     ops.linear(ctx, x.to(torch.bfloat16), lin.wf, rows, n, y, geglu=geglu, y2=y2, ln=f, algo=algo, nsplit=nsplit)
     torch.cuda.synchronize()
     assert rel(y, ref) < 1e-2
+    # per row, so that the |mean| >> std row (where rstd * (acc - mean * csum) cancels) is not diluted by the others
+    per_row = ((y.float() - ref).norm(dim=1) / ref.norm(dim=1)).max()
+    assert rel(y[5], ref[5]) < 1e-2 and per_row < 2e-2, float(per_row)
     if geglu:
         hh = ref.view(rows, n // 16, 2, 8)[:, :, 0].reshape(rows, n // 2)
         gt = ref.view(rows, n // 16, 2, 8)[:, :, 1].reshape(rows, n // 2)
@@ -478,39 +439,11 @@ def test_attention_fwd_bwd(ctx, n, t, heads, cfg, monkeypatch):
     assert rel(dq.view(n, t, 3 * C), qkv.grad) < 2e-2
 
 
-@pytest.mark.parametrize("n,t,heads", [(1, 300, 2), (2, 1000, 3), (1, 6912, 5)])
-def test_attention_fwd_stream_k(ctx, n, t, heads, monkeypatch):
-    """Stream-K forward: partial (m, l, O) of a query block's key ranges folded by the last-arriving block in
-    block order with the online-softmax rescale; bit-identical on repeat, equal to the plain grid up to
-    summation order, and against fp32 SDPA / logsumexp."""
-    from depth_completion_amd import ops
-    C = heads * 64
-    qkv = rnd(n, t, 3 * C, seed=34).to(torch.bfloat16).float()
-    q, k, v = qkv.split(C, -1)
-    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
-    ref = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
-    lse_ref = torch.logsumexp(torch.einsum("nhqd,nhkd->nhqk", sh(q), sh(k)) / 8, -1)
-    qkv_b = qkv.to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
-    outs = {}
-    for mode in ("0", "2", "2b"):
-        monkeypatch.setenv("DC_ATTN_SK_FWD", mode[0])
-        ob = torch.zeros(n * t, C, dtype=torch.bfloat16, device=dev)
-        lse = torch.zeros(n, heads, t, device=dev)
-        ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
-        torch.cuda.synchronize()
-        outs[mode] = (ob, lse)
-    assert torch.equal(outs["2"][0], outs["2b"][0]) and torch.equal(outs["2"][1], outs["2b"][1])
-    assert rel(outs["2"][0], outs["0"][0]) < 5e-3
-    assert rel(outs["2"][0].view(n, t, C), ref) < 1e-2
-    assert rel(outs["2"][1], lse_ref) < 1e-4
-
-
 @pytest.mark.parametrize("n,t,heads,peak", [(1, 64, 1, 1.0), (1, 65, 2, 1.0), (2, 300, 2, 1.0), (1, 1000, 5, 1.0),
                                             (1, 1000, 5, 6.0), (1, 6912, 5, 1.0), (1, 6912, 5, 4.0)])
-def test_attention_fwd_fastsm(ctx, n, t, heads, peak, monkeypatch):
-    """Forward softmax with the lazy rescale decided from the row sum (DC_ATTN_FASTSM=1): bit-identical on repeat,
-    equal to the max-decided form up to the reference-max choice, and against fp32 SDPA / logsumexp.  `peak` scales
-    the queries so that scores are peaked (rows whose sum crosses e^8 mid-sweep, the recompute path)."""
+def test_attention_fwd_peaked(ctx, n, t, heads, peak):
+    """Forward on peaked and unit-scale scores (`peak` scales the queries: rows whose running max moves by more than
+    the lazy-rescale slack mid-sweep): bit-identical on repeat and against fp32 SDPA / logsumexp."""
     from depth_completion_amd import ops
     C = heads * 64
     qkv = rnd(n, t, 3 * C, seed=41).to(torch.bfloat16).float()
@@ -522,113 +455,15 @@ def test_attention_fwd_fastsm(ctx, n, t, heads, peak, monkeypatch):
     lse_ref = torch.logsumexp(torch.einsum("nhqd,nhkd->nhqk", sh(q), sh(k)) / 8, -1)
     qkv_b = qkv.to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
     outs = {}
-    for mode in ("0", "1", "1b"):
-        monkeypatch.setenv("DC_ATTN_FASTSM", mode[0])
+    for mode in ("a", "b"):
         ob = torch.zeros(n * t, C, dtype=torch.bfloat16, device=dev)
         lse = torch.zeros(n, heads, t, device=dev)
         ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
         torch.cuda.synchronize()
         outs[mode] = (ob, lse)
-    assert torch.equal(outs["1"][0], outs["1b"][0]) and torch.equal(outs["1"][1], outs["1b"][1])
-    assert rel(outs["1"][0], outs["0"][0]) < 5e-3
-    assert rel(outs["1"][0].view(n, t, C), ref) < 1e-2
-    assert rel(outs["1"][1], lse_ref) < 1e-4
-
-
-@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (1, 65, 2), (1, 300, 2), (3, 257, 2), (2, 1000, 3), (1, 1728, 10),
-                                       (1, 6912, 5)])
-def test_attention_fwd_pingpong(ctx, n, t, heads, monkeypatch):
-    """Ping-pong forward (8-wave blocks, halves one segment apart, stream-K over 256-query blocks; DC_ATTN_PP=2
-    forces it at every shape): bit-identical on repeat, equal to the one-barrier-per-tile kernels up to
-    summation order, and against fp32 SDPA / logsumexp.  (1, 65, 2): a one-key last tile; (3, 257, 2): a
-    one-query last block; (1, 6912, 5) / (1, 1728, 10): the UNet level-0 / level-1 shapes of the default policy."""
-    from depth_completion_amd import ops
-    C = heads * 64
-    qkv = rnd(n, t, 3 * C, seed=35).to(torch.bfloat16).float()
-    q, k, v = qkv.split(C, -1)
-    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
-    ref = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
-    lse_ref = torch.logsumexp(torch.einsum("nhqd,nhkd->nhqk", sh(q), sh(k)) / 8, -1)
-    qkv_b = qkv.to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
-    outs = {}
-    for mode in ("0", "2", "2b"):
-        monkeypatch.setenv("DC_ATTN_PP", mode[0])
-        ob = torch.zeros(n * t, C, dtype=torch.bfloat16, device=dev)
-        lse = torch.zeros(n, heads, t, device=dev)
-        ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
-        torch.cuda.synchronize()
-        outs[mode] = (ob, lse)
-    assert torch.equal(outs["2"][0], outs["2b"][0]) and torch.equal(outs["2"][1], outs["2b"][1])
-    assert rel(outs["2"][0], outs["0"][0]) < 5e-3
-    assert rel(outs["2"][0].view(n, t, C), ref) < 1e-2
-    assert rel(outs["2"][1], lse_ref) < 1e-4
-
-
-@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (1, 65, 2), (1, 300, 2), (3, 257, 2), (2, 1000, 3), (1, 1728, 10),
-                                       (1, 6912, 5)])
-def test_attention_dq_pingpong(ctx, n, t, heads, monkeypatch):
-    """Ping-pong dQ (two 32-key steps per tile, halves one segment apart; DC_ATTN_PP_DQ=2 forces it): dQ
-    bit-identical on repeat and equal to the plain kernels up to summation order; delta (published by the key-0
-    segment) identical, so dK / dV are bitwise equal; against fp32 SDPA."""
-    from depth_completion_amd import ops
-    C = heads * 64
-    qkv = rnd(n, t, 3 * C, seed=36).to(torch.bfloat16).float().requires_grad_(True)
-    q, k, v = qkv.split(C, -1)
-    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
-    o = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
-    do = rnd(n, t, C, seed=37)
-    o.backward(do)
-    qkv_b = qkv.detach().to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
-    dob = do.to(torch.bfloat16).reshape(n * t, C)
-    ob = torch.empty(n * t, C, dtype=torch.bfloat16, device=dev)
-    lse = torch.empty(n, heads, t, device=dev)
-    ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
-    outs = {}
-    for mode in ("0", "2", "2b"):
-        monkeypatch.setenv("DC_ATTN_PP_DQ", mode[0])
-        dq = torch.zeros_like(qkv_b)
-        delta = torch.empty(n, heads, t, device=dev)
-        ops.attn_bwd(ctx, qkv_b, ob, dob, lse, n, t, heads, delta, dq)
-        torch.cuda.synchronize()
-        outs[mode] = (dq, delta)
-    assert torch.equal(outs["2"][0], outs["2b"][0])
-    assert torch.equal(outs["2"][1], outs["0"][1])
-    assert torch.equal(outs["2"][0][:, C:], outs["0"][0][:, C:])
-    assert rel(outs["2"][0][:, :C], outs["0"][0][:, :C]) < 5e-3
-    assert rel(outs["2"][0].view(n, t, 3 * C)[..., :C], qkv.grad[..., :C]) < 2e-2
-
-
-@pytest.mark.parametrize("n,t,heads", [(1, 64, 1), (1, 65, 2), (1, 300, 2), (3, 257, 2), (2, 1000, 3), (1, 1728, 10),
-                                       (1, 6912, 5)])
-def test_attention_dkdv_pingpong(ctx, n, t, heads, monkeypatch):
-    """Ping-pong dK/dV (256 keys per block unit, two 32-query steps per tile; DC_ATTN_PP_DKDV=2 forces it): dK / dV
-    bit-identical on repeat and equal to the plain kernels up to summation order, dQ untouched (bitwise), and
-    against fp32 SDPA."""
-    from depth_completion_amd import ops
-    C = heads * 64
-    qkv = rnd(n, t, 3 * C, seed=38).to(torch.bfloat16).float().requires_grad_(True)
-    q, k, v = qkv.split(C, -1)
-    sh = lambda z: z.view(n, t, heads, 64).transpose(1, 2)  # noqa: E731
-    o = F.scaled_dot_product_attention(sh(q), sh(k), sh(v)).transpose(1, 2).reshape(n, t, C)
-    do = rnd(n, t, C, seed=39)
-    o.backward(do)
-    qkv_b = qkv.detach().to(torch.bfloat16).reshape(n * t, 3 * C).contiguous()
-    dob = do.to(torch.bfloat16).reshape(n * t, C)
-    ob = torch.empty(n * t, C, dtype=torch.bfloat16, device=dev)
-    lse = torch.empty(n, heads, t, device=dev)
-    ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
-    outs = {}
-    for mode in ("0", "2", "2b"):
-        monkeypatch.setenv("DC_ATTN_PP_DKDV", mode[0])
-        dq = torch.zeros_like(qkv_b)
-        delta = torch.empty(n, heads, t, device=dev)
-        ops.attn_bwd(ctx, qkv_b, ob, dob, lse, n, t, heads, delta, dq)
-        torch.cuda.synchronize()
-        outs[mode] = dq
-    assert torch.equal(outs["2"], outs["2b"])
-    assert torch.equal(outs["2"][:, :C], outs["0"][:, :C])
-    assert rel(outs["2"][:, C:], outs["0"][:, C:]) < 5e-3
-    assert rel(outs["2"].view(n, t, 3 * C)[..., C:], qkv.grad[..., C:]) < 2e-2
+    assert torch.equal(outs["a"][0], outs["b"][0]) and torch.equal(outs["a"][1], outs["b"][1])
+    assert rel(outs["a"][0].view(n, t, C), ref) < 1e-2
+    assert rel(outs["a"][1], lse_ref) < 1e-4
 
 
 @pytest.mark.parametrize("n,t,heads", [(1, 300, 2), (2, 1000, 3), (1, 6912, 5)])

@@ -19,6 +19,10 @@ from oracle.diffusers_ref import (AutoencoderTiny, DDIMScheduler, UNet2DConditio
 
 pytestmark = pytest.mark.gpu
 dev = torch.device("cuda:0")
+# The oracle legs of the tiny-UNet cases run on the host CPU: deterministic from run to run, so the bf16 leg's error
+# (the anchor of every relative bound below) is one fixed number per host, not a sample of PyTorch-ROCm's
+# run-to-run spread (its GPU conv backward and SDPA are not deterministic)
+ORACLE = torch.device("cpu")
 
 
 def synth_inputs(n, h, w, n_points, seed):
@@ -73,13 +77,15 @@ def test_pipeline_parity(which, n, h, w, res, steps):
     eh, ew = -(-(res * h // max(h, w)) // 8), -(-(res * w // max(h, w)) // 8)
     noise = torch.randn((1, 4, eh, ew), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
     kw = dict(norm="const", steps=steps, resolution=res, init_noise=noise)
-    o32, usd, vsd, emb = build(cfg_o, hcfg, torch.float32, dev)
-    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **kw)
-    o16, *_ = build(cfg_o, hcfg, torch.bfloat16, dev)
-    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **kw)
+    od = ORACLE if which == "tiny" else dev
+    o32, usd, vsd, emb = build(cfg_o, hcfg, torch.float32, od)
+    d32, l32 = o32(imgs.to(od), sparses.to(od), 120.0, **kw)
+    o16, *_ = build(cfg_o, hcfg, torch.bfloat16, od)
+    d16, l16 = o16(imgs.to(od), sparses.to(od), 120.0, **kw)
     pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=hcfg, device=dev)
     dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **kw)
     torch.cuda.synchronize()
+    dh, lh, d32, l32, d16, l16 = (t.cpu() for t in (dh, lh, d32, l32, d16, l16))
     assert dh.shape == (n, 1, h, w) and lh.shape == (n, 4, eh, ew) and lh.dtype == torch.bfloat16
     assert torch.isfinite(dh).all()
     mean_h, p99_h = fitted_error(dh, d32, sparses)
@@ -146,13 +152,14 @@ def test_plain_ddim_closed_form(kw):
     imgs, sparses = synth_inputs(n, h, w, 60, seed=17)
     noise = torch.randn((1, 4, 6, 8), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
     args = dict(kw, steps=steps, resolution=res, init_noise=noise, train_latents=False)
-    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
-    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
-    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
-    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, ORACLE)
+    d32, l32 = o32(imgs, sparses, 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, ORACLE)
+    d16, l16 = o16(imgs, sparses, 120.0, **args)
     pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
     dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
     torch.cuda.synchronize()
+    dh, lh = dh.cpu(), lh.cpu()
     assert torch.isfinite(dh).all()
     rng = (d32.amax(dim=(1, 2, 3)) - d32.amin(dim=(1, 2, 3))).view(-1, 1, 1, 1)
     err_h = float(((dh - d32).abs() / rng).mean())
@@ -171,13 +178,14 @@ def _mode_parity(args, seed, label, fitted=False, d_factor=2.0, d_abs=0.0):
     imgs, sparses = synth_inputs(n, h, w, 60, seed=seed)
     noise = torch.randn((1, 4, 6, 8), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
     args = dict(args, resolution=res, init_noise=noise)
-    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
-    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
-    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
-    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, ORACLE)
+    d32, l32 = o32(imgs, sparses, 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, ORACLE)
+    d16, l16 = o16(imgs, sparses, 120.0, **args)
     pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
     dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
     torch.cuda.synchronize()
+    dh, lh = dh.cpu(), lh.cpu()
     assert torch.isfinite(dh).all() and dh.shape == d32.shape and lh.shape == l32.shape
     lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
     lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
@@ -259,23 +267,23 @@ def test_nearest_interp(kw):
     eh, ew = -(-(res * h // max(h, w)) // 8), -(-(res * w // max(h, w)) // 8)
     noise = torch.randn((1, 4, eh, ew), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
     args = dict(kw, norm="const", steps=5, resolution=res, init_noise=noise, interp_mode="nearest")
-    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
-    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
-    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
-    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, ORACLE)
+    d32, l32 = o32(imgs, sparses, 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, ORACLE)
+    d16, l16 = o16(imgs, sparses, 120.0, **args)
     pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
     dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
     torch.cuda.synchronize()
+    dh, lh = dh.cpu(), lh.cpu()
     assert dh.shape == d32.shape and torch.isfinite(dh).all()
     err_h, _ = fitted_error(dh, d32, sparses)
     err_b, _ = fitted_error(d16, d32, sparses)
     lat_h = float((lh.float() - l32.float()).norm() / l32.float().norm())
     lat_b = float((l16.float() - l32.float()).norm() / l32.float().norm())
     print(f"\nnearest {kw}: HIP |d| {err_h:.5f} latent {lat_h:.4f} | oracle-bf16 |d| {err_b:.5f} latent {lat_b:.4f}")
-    # the oracle's own bf16 |d| error is one sample of a spread (train_latents=False: 0.006 - 0.027 across GPU runs,
-    # profiles/r03_suite, r03v, r03z, r04za -- torch's bf16 GPU path is not run-to-run deterministic), so the depth
-    # bound takes it no lower than 0.01; the latent bound stays relative
-    assert err_h <= 2 * max(err_b, 0.01) + 2e-3 and lat_h <= 2 * lat_b + 2e-3
+    # (the bf16 anchor runs on the host CPU: on PyTorch-ROCm's GPU path its error spread 0.006 - 0.027 between runs,
+    # profiles/r04za, which a relative bound cannot take)
+    assert err_h <= 2 * err_b + 2e-3 and lat_h <= 2 * lat_b + 2e-3
     # blocky: every output pixel equals one decoded pixel, so the dense map has at most PH*PW levels per frame
     assert dh.unique().numel() <= 48 * 64
 
@@ -320,10 +328,10 @@ def test_sparse_aware_decode(kw, res, monkeypatch):
     imgs, sparses = synth_inputs(n, h, w, 40, seed=34)
     noise = torch.randn((1, 4, ph // 8, pw // 8), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
     args = dict(kw, norm="const", steps=4, resolution=res, init_noise=noise)
-    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
-    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
-    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
-    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, ORACLE)
+    d32, l32 = o32(imgs, sparses, 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, ORACLE)
+    d16, l16 = o16(imgs, sparses, 120.0, **args)
     out = {}
     for mode in ("1", "0"):
         monkeypatch.setenv("DC_SPARSE_DECODE", mode)
@@ -332,7 +340,7 @@ def test_sparse_aware_decode(kw, res, monkeypatch):
         st = pipe._plans[(1, ph // 8, pw // 8)]
         assert (st["graph_key"][-1] != ()) == (mode == "1")   # the row sets were used / not used
     torch.cuda.synchronize()
-    (dh, lh), (dd, ld_) = out["1"], out["0"]
+    (dh, lh), (dd, ld_) = [(a.cpu(), b.cpu()) for a, b in (out["1"], out["0"])]
     lat = lambda a: float((a.float() - l32.float()).norm() / l32.float().norm())  # noqa: E731
     err_h, _ = fitted_error(dh, d32, sparses)
     err_b, _ = fitted_error(d16, d32, sparses)
@@ -381,12 +389,13 @@ def test_vae_original(kw):
         vae = AutoencoderKL(ocfg)
         vae.load_state_dict(ksd)
         emb = synthetic_text_embedding(13, cfg_o.cross_attention_dim)
-        o = P.OracleMarigoldDC(unet.to(dt).to(dev), vae.to(dt).to(dev), DDIMScheduler(), emb, dtype=dt, device=dev)
-        outs[dt] = o(imgs.to(dev), sparses.to(dev), 120.0, **args)
+        o = P.OracleMarigoldDC(unet.to(dt), vae.to(dt), DDIMScheduler(), emb, dtype=dt, device=ORACLE)
+        outs[dt] = o(imgs, sparses, 120.0, **args)
     pipe = MarigoldDepthCompletionPipeline(usd, ksd, emb, unet_config=TINY, device=dev, vae="original",
                                            vae_config=TINY_KL)
     dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
     torch.cuda.synchronize()
+    dh, lh = dh.cpu(), lh.cpu()
     (d32, l32), (d16, l16) = outs[torch.float32], outs[torch.bfloat16]
     assert dh.shape == d32.shape and torch.isfinite(dh).all()
     err_h, _ = fitted_error(dh, d32, sparses)
@@ -424,13 +433,14 @@ def test_baseline_config_shapes(h, w, npts, density):
     noise = torch.randn((1, 4, eh, ew), generator=torch.Generator().manual_seed(2024), dtype=torch.bfloat16)
     args = dict(norm="const", steps=3, resolution=res, init_noise=noise)
     cfg_o = tiny_unet_config()
-    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, dev)
-    d32, l32 = o32(imgs.to(dev), sparses.to(dev), 120.0, **args)
-    o16, *_ = build(cfg_o, TINY, torch.bfloat16, dev)
-    d16, l16 = o16(imgs.to(dev), sparses.to(dev), 120.0, **args)
+    o32, usd, vsd, emb = build(cfg_o, TINY, torch.float32, ORACLE)
+    d32, l32 = o32(imgs, sparses, 120.0, **args)
+    o16, *_ = build(cfg_o, TINY, torch.bfloat16, ORACLE)
+    d16, l16 = o16(imgs, sparses, 120.0, **args)
     pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
     dh, lh = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
     torch.cuda.synchronize()
+    dh, lh, d32, l32, d16, l16 = (t.cpu() for t in (dh, lh, d32, l32, d16, l16))
     assert dh.shape == (1, 1, h, w) and lh.shape == (1, 4, eh, ew) and torch.isfinite(dh).all()
     err_h, p99_h = fitted_error(dh, d32, sparses)
     err_b, p99_b = fitted_error(d16, d32, sparses)

@@ -1,9 +1,9 @@
 """Attention fwd/bwd microbenchmark at the UNet shapes (GPU). DC_ATTN_CFG=<i> forces a block configuration.
 
-The forward / backward are timed with the ping-pong forward / backward kernels off and on (DC_ATTN_PP, DC_ATTN_PP_DQ + DC_ATTN_PP_DKDV = 0 / 2 (forced wherever it fits),
-alternating, `--reps` pairs)."""
+A/B between two builds: run it once per library with DC_LIB=<path to libdcamd.so> (tools/ab/lib_ab.sh), alternating.
+Per shape: forward, and dQ + dK/dV (the backward), best of --reps timed loops of 10 calls each.
+"""
 import argparse
-import os
 import sys
 
 import torch
@@ -15,7 +15,6 @@ from depth_completion_amd.ops import Ctx  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--no-bwd", action="store_true")
-ap.add_argument("--env", default="DC_ATTN_PP", help="forward A/B switch (0 vs 2): DC_ATTN_PP or DC_ATTN_FASTSM")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 ctx = Ctx(dev)
@@ -43,23 +42,12 @@ for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (8, 6912, 5), (8,
     dq = torch.empty_like(qkv)
     delta = torch.empty(n, heads, t, device=dev)
     f = 4.0 * n * t * t * 64 * heads
-    res = {"0": [], "2": []}
-    for _ in range(args.reps):
-        for mode in ("0", "2"):
-            os.environ[args.env] = mode
-            res[mode].append(timed(lambda: ops.attn_fwd(ctx, qkv, n, t, heads, o, lse)))
-    for mode, name in (("0", "fwd"), ("2", f"fwd-{args.env}")):
-        ms = min(res[mode])
-        print(f"n={n} T={t} H={heads} {name}: {ms*1e3:.1f} us  {f/ms/1e9:.0f} TF/s  (all: "
-              f"{' '.join(f'{x*1e3:.1f}' for x in res[mode])})", flush=True)
+    fw = [timed(lambda: ops.attn_fwd(ctx, qkv, n, t, heads, o, lse)) for _ in range(args.reps)]
+    ms = min(fw)
+    print(f"n={n} T={t} H={heads} fwd: {ms*1e3:.1f} us  {f/ms/1e9:.0f} TF/s  (all: {' '.join(f'{x*1e3:.1f}' for x in fw)})",
+          flush=True)
     if not args.no_bwd:
-        rb = {"0": [], "2": []}
-        for _ in range(args.reps):
-            for mode in ("0", "2"):
-                os.environ["DC_ATTN_PP_DQ"] = mode
-                os.environ["DC_ATTN_PP_DKDV"] = mode
-                rb[mode].append(timed(lambda: ops.attn_bwd(ctx, qkv, o, do, lse, n, t, heads, delta, dq)))
-        for mode, name in (("0", "bwd"), ("2", "bwd-pp")):
-            ms = min(rb[mode])
-            print(f"n={n} T={t} H={heads} {name}: {ms*1e3:.1f} us  {3.5*f/ms/1e9:.0f} TF/s (algorithmic incl. recompute)"
-                  f"  (all: {' '.join(f'{x*1e3:.1f}' for x in rb[mode])})", flush=True)
+        bw = [timed(lambda: ops.attn_bwd(ctx, qkv, o, do, lse, n, t, heads, delta, dq)) for _ in range(args.reps)]
+        ms = min(bw)
+        print(f"n={n} T={t} H={heads} bwd: {ms*1e3:.1f} us  {3.5*f/ms/1e9:.0f} TF/s (algorithmic incl. recompute)"
+              f"  (all: {' '.join(f'{x*1e3:.1f}' for x in bw)})", flush=True)

@@ -10,9 +10,11 @@
 #   file=<test file(s)>        the GPU tests of these files
 #   smoke                      __graft_entry__.smoke()
 #   c2 | c2cpu                 C2 bench line (c2cpu: with the CPU baseline)
+#   c2at=<dir>                 C2 bench line of the tree copy in <dir> (A/B arm)
 #   c3 | c4 | c4b8 | c5        C3 batch 8, C4 KITTI 64-beam (batch 1 / 8), C5 10-seed ensemble bench lines
 #   trace                      rocprofv3 --kernel-trace --stats of a short C2 bench
 #   trace3                     the same for C3 (batch 8)
+#   calltrace                  kernel trace of 4 C2 calls, itemised outside the step graphs (tools/call_timeline.py)
 #   pmc | pmc8                 FETCH_SIZE, WRITE_SIZE, MFMA-busy passes over the conv kernels (eager C2 / C3, 4 steps)
 #   breakdown[=<batch>]        per-shape conv breakdown of one guided step (tools/conv_breakdown.py)
 #   stepprof                   per-shape conv time inside the graph-replayed step (tools/step_profile.py)
@@ -41,7 +43,12 @@ for step in "$@"; do
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 ;;
     c2)
-      timeout -k 10 400 python -u bench.py --no-cpu-baseline > "$out/bench_c2.json" 2> "$out/bench_c2.err" ;;
+      timeout -k 10 400 python -u bench.py --no-cpu-baseline > "$out/bench_c2.json" 2> "$out/bench_c2.err"
+      cp "$out/bench_c2.json" "$out/bench_c2_$n.json" ;;
+    c2at=*)
+      # the C2 bench line of another tree (an A/B arm: a full copy of a tree with its built library, e.g. ab/old)
+      d=${step#c2at=}
+      (cd "$d" && timeout -k 10 400 python -u bench.py --no-cpu-baseline) > "$out/bench_c2_$n.json" 2> "$out/bench_c2_$n.err" ;;
     c2cpu)
       timeout -k 10 600 python -u bench.py > "$out/bench_c2.json" 2> "$out/bench_c2.err" ;;
     c3)
@@ -59,6 +66,11 @@ for step in "$@"; do
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- \
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$out/trace_bench.json" 2> "$out/trace.err" ;;
+    calltrace)
+      # per-call time outside the step graphs (tools/call_timeline.py): 4 calls, 3 stretches between them
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$out/calltrace" -o run --output-format csv -- \
+        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$out/calltrace_bench.json" 2> "$out/calltrace.err"
+      python3 tools/call_timeline.py "$out/calltrace/run_kernel_trace.csv" > "$out/call_timeline.txt" 2>&1 ;;
     trace3)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace3" -o run --output-format csv -- \
         python3 bench.py --batch 8 --steps 1 --warmup 1 --no-cpu-baseline > "$out/trace3_bench.json" 2> "$out/trace3.err" ;;
