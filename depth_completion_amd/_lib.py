@@ -11,7 +11,7 @@ from pathlib import Path
 
 # DC_LIB overrides the in-tree library (A/B experiments between builds); there is still no fallback
 _LIB_PATH = Path(os.environ.get("DC_LIB") or Path(__file__).resolve().parent / "libdcamd.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -57,7 +57,7 @@ class ConvDesc(C.Structure):
         ("ws", vp), ("ws_bytes", i64),
         ("geglu", i32), ("y2", vp), ("ldy2", i32), ("aux", vp), ("ldaux", i32),
         ("algo", i32), ("splitk", i32), ("rows", vp), ("nrows", i32), ("gn", C.POINTER(GnFuse)),
-        ("ln", C.POINTER(LnFuse)),
+        ("ln", C.POINTER(LnFuse)), ("geglu_n", i32),
     ]
 
 
@@ -134,6 +134,7 @@ _SIGS.update({
     "dc_schedule_tables": [i32, C.c_double, C.c_double, i32, vp, vp, vp],
     "dc_timestep_embedding": [vp, i32, i32, vp],
     "dc_fold_cross_attention": [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+    "dc_fold_linear_pair": [vp, vp, i32, i32, vp, vp, vp, vp, vp],
     "dc_fold_layernorm": [vp, i32, i32, vp, vp, vp, vp, vp, vp],
     "dc_conv_pick": [vp, vp, i32, vp, vp],
     "dc_sample_params_default": [vp],

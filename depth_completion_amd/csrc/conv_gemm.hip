@@ -15,9 +15,9 @@ static_assert(kNumAll + kNumSkinny + kNumResident + 1 == kWideFirst, "external a
 constexpr int kNumExt = kHaloXFirst + kNumHaloX - 1;
 extern "C" int dc_conv_num_algos(void) { return kNumExt; }
 
-extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
+// the kernel parameters of a descriptor, checked (DC_OK or the error status); M = output rows
+static int conv_params(const dc_conv_desc* d, ConvGemmParams& p, long& M_out) {
   if (!d || !d->x || !d->w || !d->y) return DC_ERR_ARG;
-  ConvGemmParams p;
   p.x = (const bf16*)d->x;
   p.x2 = (const bf16*)(d->x2 ? d->x2 : d->x);
   p.ldx = d->ldx;
@@ -37,6 +37,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   p.ws_bytes = d->ws_bytes < (1L << 31) ? d->ws_bytes : (1L << 31);  // 32-bit buffer offsets
   p.splits = 1; p.kps = 0; p.counters = nullptr; p.sk_blocks = 0;
   p.geglu = d->geglu;
+  p.geglu_n = d->geglu_n;
   p.y2 = (bf16*)d->y2; p.ldy2 = d->ldy2;
   p.aux = (const bf16*)d->aux; p.ldaux = d->ldaux;
   p.rows = d->rows; p.nrows = d->rows ? d->nrows : 0;
@@ -54,7 +55,13 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   if (p.geglu) {  // plain linear / conv output only: no residual, mask, row bias or activation
     if (p.resid || p.mask || p.rowbias || p.act || p.cout % 16) return DC_ERR_ARG;
     if (p.geglu == 1 && (!p.y2 || p.ldy2 % 8 || ((uintptr_t)p.y2 & 15))) return DC_ERR_ARG;
-    if (p.geglu == 2 && (!p.aux || p.ldaux % 8 || ((uintptr_t)p.aux & 15) || p.ldy < 2 * p.cout)) return DC_ERR_ARG;
+    const int gn_cols = (p.geglu == 2 && p.geglu_n) ? p.geglu_n : p.cout;   // the GEGLU-backward columns
+    if (p.geglu == 2 && (!p.aux || p.ldaux % 8 || ((uintptr_t)p.aux & 15) || p.ldy < 2 * gn_cols)) return DC_ERR_ARG;
+    if (p.geglu_n && (p.geglu != 2 || p.geglu_n < 0 || p.geglu_n >= p.cout || p.geglu_n % 256 || !p.y2 ||
+                      p.ldy2 % 8 || ((uintptr_t)p.y2 & 15) || p.ldy2 < p.cout - p.geglu_n))
+      return DC_ERR_ARG;
+  } else if (p.geglu_n) {
+    return DC_ERR_ARG;
   }
   // shape / alignment contract (host pads channels, see DESIGN.md "layouts")
   if (p.ktot % 64 != 0 || p.ktot < p.kh * p.kw * p.cin) return DC_ERR_ARG;
@@ -81,6 +88,7 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
   make_fast_div((unsigned)p.wout, p.w_mul, p.w_shr);
   make_fast_div((unsigned)p.hout, p.h_mul, p.h_shr);
   const long M = p.rows ? p.nrows : (long)p.nb * p.hout * p.wout;
+  M_out = M;
   memset(&p.gn, 0, sizeof p.gn);
   if (d->gn) {
     // fused GroupNorm statistics: whole 8-channel vectors, every output row in a whole frame of each target
@@ -121,11 +129,19 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
       p.gn.silu = g.silu ? 1 : 0;
     }
   }
-  hipStream_t s = (hipStream_t)stream;
-  int algo = d->algo, splits = d->splitk;
   p.ln_csum = nullptr;
   p.ln_cbias = nullptr;
   p.ln_stats = nullptr;
+  return DC_OK;
+}
+
+extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
+  ConvGemmParams p;
+  long M = 0;
+  if (const int st = conv_params(d, p, M)) return st;
+  const bool smallc = (p.cin % 64) != 0;
+  hipStream_t s = (hipStream_t)stream;
+  int algo = d->algo, splits = d->splitk;
   if (d->ln) {
     // LayerNorm folded in (dc_ln_fuse): a linear on an im2col tile (split-K / stream-K allowed: the epilogue
     // applies the row statistics to the summed tile)

@@ -73,6 +73,7 @@ struct ConvGemmParams {
   int* counters;        // [tiles] arrival counts, zero between launches (the workspace starts zeroed)
   int sk_blocks;        // > 0: stream-K over this many blocks (split-K / plain tiles: 0)
   int geglu;            // GEGLU epilogue (include/dcamd.h): 0 none, 1 fwd (interleaved h/gate), 2 bwd
+  int geglu_n;          // geglu 2: columns >= geglu_n (> 0) are stored plainly into y2 (dc_fold_linear_pair's dgrad)
   bf16* y2;
   int ldy2;
   const bf16* aux;
@@ -947,6 +948,20 @@ __device__ __forceinline__ void tile_epilogue(const ConvGemmParams& p, char* sme
 #pragma unroll
       for (int k = 0; k < 8; ++k) o[k] = h[k] * (float)(bf16)gelu_f(gt[k]);
       store8(p.y2 + m * p.ldy2 + c / 2, o);
+    }
+    return;
+  }
+  if (p.geglu == 2 && p.geglu_n && n0 >= p.geglu_n) {
+    // the residual half of the folded FF2 / proj_out input-gradient: plain columns into y2 (block-uniform: geglu_n is
+    // a multiple of 256, every tile lies on one side)
+    for (int g = lane; g < WM * GPR; g += 64) {
+      const int row = g / GPR, cg = g - (g / GPR) * GPR;
+      const long m = m0 + wm * WM + row;
+      const int c = n0 + wn * WN + cg * 8;
+      if (m >= M || c >= p.cout) continue;
+      float v[8];
+      load8(es + row * LDE + cg * 8, v);
+      store8(p.y2 + m * p.ldy2 + (c - p.geglu_n), v);
     }
     return;
   }

@@ -7,10 +7,13 @@
 //   dc_timestep_embedding    diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), fp32
 //   dc_fold_cross_attention  attn2 with the constant 2-token empty-prompt context folded to (U, D, c0)
 //   dc_fold_layernorm        a LayerNorm folded into the linear that consumes it (include/dcamd.h dc_ln_fuse)
+//   dc_fold_linear_pair      FF2 and proj_out of a transformer block folded into one two-source linear
 //   dc_conv_pick             the tuned GEMM variant of a conv shape, nearest tuned shape for shapes not in the table
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../../include/dcamd.h"
@@ -121,6 +124,53 @@ extern "C" int dc_fold_layernorm(const float* w, int cout, int k, const float* g
     csum[n] = (float)cs;
     cbias[n] = (float)(cb + (bias ? (double)round_bf16(bias[n]) : 0.0));
   }
+  return 0;
+}
+
+extern "C" int dc_fold_linear_pair(const float* w2, const float* b2, int c, int k2, const float* wp, const float* bp,
+                                   void* wf, void* wd, float* bias) {
+  if (!w2 || !b2 || !wp || !bp || !wf || !wd || !bias || c <= 0 || k2 <= 0) return 1;
+  const int kt = k2 + c;
+  uint16_t* of = static_cast<uint16_t*>(wf);
+  uint16_t* od = static_cast<uint16_t*>(wd);
+  auto bits = [](float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (uint16_t)(u >> 16);
+  };
+  std::vector<double> w2d((size_t)c * k2);
+  for (size_t e = 0; e < w2d.size(); ++e) w2d[e] = (double)round_bf16(w2[e]);
+  auto rows = [&](int r0, int r1) {
+    std::vector<double> acc((size_t)k2);
+    for (int i = r0; i < r1; ++i) {   // row i of Wp W2: sum_m Wp[i][m] W2[m][.], m ascending
+      std::fill(acc.begin(), acc.end(), 0.0);
+      for (int m = 0; m < c; ++m) {
+        const double a = (double)round_bf16(wp[(size_t)i * c + m]);
+        const double* w2m = w2d.data() + (size_t)m * k2;
+        for (int j = 0; j < k2; ++j) acc[j] += a * w2m[j];
+      }
+      for (int j = 0; j < k2; ++j) {
+        const uint16_t b = bits(round_bf16((float)acc[j]));
+        of[(size_t)i * kt + j] = b;
+        od[(size_t)j * c + i] = b;
+      }
+      for (int j = 0; j < c; ++j) {
+        const uint16_t b = bits(round_bf16(wp[(size_t)i * c + j]));
+        of[(size_t)i * kt + k2 + j] = b;
+        od[(size_t)(k2 + j) * c + i] = b;
+      }
+      double bb = (double)round_bf16(bp[i]);
+      for (int m = 0; m < c; ++m) bb += (double)round_bf16(wp[(size_t)i * c + m]) * (double)round_bf16(b2[m]);
+      bias[i] = (float)bb;
+    }
+  };
+  const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) {
+    const int r0 = (int)((long)c * t / nt), r1 = (int)((long)c * (t + 1) / nt);
+    if (r1 > r0) th.emplace_back(rows, r0, r1);
+  }
+  for (auto& x : th) x.join();
   return 0;
 }
 

@@ -253,6 +253,24 @@ class Loader {
     l.cbias = mem_.upload(cb);
     return l;
   }
+  // weights.FoldedPair: FF2 and proj_out as one two-source linear over [gg | r2] (the shared host routine
+  // dc_fold_linear_pair); wf [c][k2 + c], wd [k2 + c][c], bias fp32
+  LinearW linear_pair(const std::string& ff2, const std::string& proj_out) {
+    HostTensor w2 = st_.get(ff2 + ".weight"), b2 = st_.get(ff2 + ".bias");
+    HostTensor wp = st_.get(proj_out + ".weight"), bp = st_.get(proj_out + ".bias");
+    LinearW l;
+    const int c = (int)w2.shape[0], k2 = (int)w2.shape[1];
+    l.cout = c;
+    l.cin = k2 + c;
+    std::vector<uint16_t> wf((size_t)c * (k2 + c)), wd((size_t)(k2 + c) * c);
+    std::vector<float> bias(c);
+    DCK(dc_fold_linear_pair(w2.data.data(), b2.data.data(), c, k2, wp.data.data(), bp.data.data(), wf.data(),
+                            wd.data(), bias.data()));
+    l.wf = mem_.upload(wf);
+    l.wd = mem_.upload(wd);
+    l.bias = mem_.upload(bias);
+    return l;
+  }
   LinearW linear(const std::string& pre, bool has_bias, bool dgrad = true) {
     HostTensor w = st_.get(pre + ".weight");
     HostTensor b;
@@ -313,8 +331,14 @@ struct Exec {
     int nrows = 0;
     const dc_gn_fuse* gn = nullptr;   // fused GroupNorm statistics (unet.py _gnf / _gn_bwd_fuse)
     const dc_ln_fuse* ln = nullptr;   // LayerNorm folded in (unet.py ln_fuse)
+    int geglu_n = 0;                  // GEGLU backward on the first geglu_n columns only (the folded FF2 / proj_out)
   };
   void conv(const Conv& a) {
+    const dc_conv_desc d = desc(a);
+    DCK(dc_conv_gemm(&d, stream));
+  }
+  // the descriptor of one call, its variant chosen as ops.conv_desc chooses it
+  dc_conv_desc desc(const Conv& a) {
     dc_conv_desc d;
     memset(&d, 0, sizeof d);
     d.x = a.x.p;
@@ -347,6 +371,7 @@ struct Exec {
     d.ws_bytes = ws_bytes;
     d.gn = a.gn;
     d.ln = a.ln;
+    d.geglu_n = a.geglu_n;
     if (a.rows) {
       d.rows = a.rows;
       d.nrows = a.nrows;
@@ -369,12 +394,17 @@ struct Exec {
       d.algo = it->second.first;
       d.splitk = it->second.second;
     }
-    DCK(dc_conv_gemm(&d, stream));
+    return d;
   }
   // ops.linear
   void linear(RB x, const void* w, int k, int rows, int cout, RB y, const float* bias = nullptr, RB resid = RB(),
               const void* rowbias = nullptr, int rowbias_ld = 0, int geglu = 0, RB y2 = RB(), RB aux = RB(),
               const dc_gn_fuse* gn = nullptr, const dc_ln_fuse* ln = nullptr) {
+    conv(lin(x, w, k, rows, cout, y, bias, resid, rowbias, rowbias_ld, geglu, y2, aux, gn, ln));
+  }
+  static Conv lin(RB x, const void* w, int k, int rows, int cout, RB y, const float* bias = nullptr, RB resid = RB(),
+                  const void* rowbias = nullptr, int rowbias_ld = 0, int geglu = 0, RB y2 = RB(), RB aux = RB(),
+                  const dc_gn_fuse* gn = nullptr, const dc_ln_fuse* ln = nullptr) {
     Conv a;
     a.x = x;
     a.nb = 1; a.hin = 1; a.win = rows; a.cin = k; a.hout = 1; a.wout = rows; a.cout = cout;
@@ -391,7 +421,7 @@ struct Exec {
     a.aux = aux;
     a.gn = gn;
     a.ln = ln;
-    conv(a);
+    return a;
   }
   void groupnorm(RB x, int nb, int hw, int c, const NormW& n, bool silu, RB y, float* stats, RB x2 = RB(),
                  int c1 = 0) {
@@ -468,7 +498,8 @@ struct ResnetW {
 struct TransformerW {
   int heads = 0, c = 0;
   NormW norm, ln1, ln2, ln3;
-  LinearW proj_in, proj_out, qkv, out, ff1, ff2;
+  LinearW proj_in, qkv, out, ff1;
+  LinearW ffo;   // ff.net.2 + proj_out folded into one linear over [gg | r2] (dc_fold_linear_pair)
   float *U = nullptr, *D = nullptr, *c0 = nullptr;
   void* tabs = nullptr;  // MFMA operand tables of the folded cross-attention (dc_crossattn_prepare)
 };
@@ -518,7 +549,6 @@ TransformerW load_transformer(Loader& L, const std::string& pre, int heads, cons
   t.heads = heads;
   t.norm = L.norm(pre + "norm", 1e-6f);
   t.proj_in = L.linear(pre + "proj_in", true);
-  t.proj_out = L.linear(pre + "proj_out", true);
   const std::string b = pre + "transformer_blocks.0.";
   t.ln1 = L.norm(b + "norm1", 1e-5f);
   t.ln2 = L.norm(b + "norm2", 1e-5f);
@@ -564,7 +594,7 @@ TransformerW load_transformer(Loader& L, const std::string& pre, int heads, cons
       }
   }
   t.ff1 = L.linear_ln_from(std::move(f1p), f1bp.data(), b + "norm3", 1e-5f);   // norm3 folded
-  t.ff2 = L.linear(b + "ff.net.2", true);
+  t.ffo = L.linear_pair(b + "ff.net.2", pre + "proj_out");
   t.c = t.proj_in.cout;
   return t;
 }
@@ -663,6 +693,12 @@ class UNetPlan {
   std::map<const void*, std::unique_ptr<dc_gn_fuse>> gn_fuse_;        // built at the first call
   std::vector<std::unique_ptr<dc_gn_fuse>> gn_bwd_;                     // backward fuses (fixed at build)
 
+  // unet.py _conv_fwd: a forward conv producing a.y, with the fused GroupNorm statistics of y's consumers
+  void conv_fwd(Exec::Conv a) {
+    a.gn = gnf(a.y);
+    ex_.conv(a);
+  }
+
   long long* gn_acc() {   // a GroupNorm site the arena was not sized for: fail, never hand out past its end
     if ((size_t)(gn_next_ + 1) * gn_words_ * 8 > gn_arena_bytes_)
       throw DcError(kErrArg, "GroupNorm accumulator arena exhausted (" + std::to_string(gn_next_) + " slots)");
@@ -746,8 +782,7 @@ class UNetPlan {
       a.x = g1; a.nb = nb; a.hin = hh; a.win = ww; a.cin = cin; a.hout = hh; a.wout = ww; a.cout = cout;
       a.w = rp->c1.wf; a.ktot = rp->c1.ktot_f; a.bias = rp->c1.bias; a.rowbias = rp->temb_table; a.rowbias_ld = cout;
       a.y = h1;
-      a.gn = gnf(h1);
-      ex.conv(a);
+      conv_fwd(a);
       gn_fwd(h1, hh * ww, cout, rp->n2, true, acc2, g2, st2);
       RB res = x;
       if (rp->has_sc) {
@@ -761,8 +796,7 @@ class UNetPlan {
       Exec::Conv b;
       b.x = g2; b.nb = nb; b.hin = hh; b.win = ww; b.cin = cout; b.hout = hh; b.wout = ww; b.cout = cout;
       b.w = rp->c2.wf; b.ktot = rp->c2.ktot_f; b.bias = rp->c2.bias; b.resid = res; b.y = out;
-      b.gn = gnf(out);
-      ex.conv(b);
+      conv_fwd(b);
     });
     TapeEntry e;
     e.kind = "resnet";
@@ -787,7 +821,7 @@ class UNetPlan {
     float* probs = fbuf((long)P * H);
     float* sl3 = fbuf((long)P * 2);
     const dc_ln_fuse lnf3{t.ff1.csum, t.ff1.cbias, sl3};   // norm3 folded into ff.net.0.proj (unet.py ln_fuse)
-    RB f8 = buf(P, 8 * C), gg = buf(P, 4 * C), r3 = buf(P, C), out = buf(P, C);
+    RB f8 = buf(P, 8 * C), gg = buf(P, 4 * C), out = buf(P, C);
     TransformerW* tp = &t;
     Exec& ex = ex_;
     long long* acc0 = gn_consumer(x, C, T);
@@ -801,9 +835,11 @@ class UNetPlan {
       DCK(dc_crossattn_fwd(r1.p, r1.ld, P, C, H, tp->ln2.eps, tp->ln2.gamma, tp->ln2.beta, tp->tabs, tp->c0, r2.p,
                            r2.ld, sl2, probs, sl3, tp->ln3.eps, ex.stream));
       ex.linear(r2, tp->ff1.wf, tp->ff1.cin, P, 8 * C, f8, nullptr, RB(), nullptr, 0, 1, gg, RB(), nullptr, &lnf3);
-      ex.linear(gg, tp->ff2.wf, tp->ff2.cin, P, C, r3, tp->ff2.bias, r2);
-      ex.linear(r3, tp->proj_out.wf, tp->proj_out.cin, P, C, out, tp->proj_out.bias, x, nullptr, 0, 0, RB(), RB(),
-                gnf(out));
+      // (FF2 + residual) -> proj_out + residual as one linear over [gg | r2] (unet.py, t.ffo)
+      Exec::Conv fo = Exec::lin(gg, tp->ffo.wf, tp->ffo.cin, P, C, out, tp->ffo.bias, x);
+      fo.x2 = r2;
+      fo.c1 = 4 * C;
+      conv_fwd(fo);
     });
     TapeEntry e;
     e.kind = "transformer";
@@ -824,8 +860,7 @@ class UNetPlan {
       Exec::Conv a;
       a.x = x; a.nb = nb; a.hin = hh; a.win = ww; a.cin = c->cin; a.hout = ho; a.wout = wo; a.cout = c->cout;
       a.stride = 2; a.w = c->wf; a.ktot = c->ktot_f; a.bias = c->bias; a.y = out;
-      a.gn = gnf(out);
-      ex.conv(a);
+      conv_fwd(a);
     });
     TapeEntry e;
     e.kind = "down";
@@ -847,8 +882,7 @@ class UNetPlan {
       Exec::Conv a;
       a.x = x; a.nb = nb; a.hin = hh; a.win = ww; a.cin = c->cin; a.hout = ho; a.wout = wo; a.cout = c->cout;
       a.mode = 1; a.w = c->wf; a.ktot = c->ktot_f; a.bias = c->bias; a.y = out;
-      a.gn = gnf(out);
-      ex.conv(a);
+      conv_fwd(a);
     });
     TapeEntry e;
     e.kind = "up";
@@ -1077,8 +1111,10 @@ class UNetPlan {
     Exec& ex = ex_;
     auto f0 = gn_bwd_fuse(x, T, C, t->norm, false, st0);
     bwd_.push_back([=, &ex]() {
-      ex.linear(dout, t->proj_out.wd, t->proj_out.cout, P, C, dr3);
-      ex.linear(dr3, t->ff2.wd, t->ff2.cout, P, 4 * C, df, nullptr, RB(), nullptr, 0, 2, RB(), f8);
+      // dL/dgg (+ GEGLU backward) into df and dL/dr2 into dr3 from the folded linear's input-gradient (unet.py)
+      Exec::Conv fb = Exec::lin(dout, t->ffo.wd, C, P, 5 * C, df, nullptr, RB(), nullptr, 0, 2, dr3, f8);
+      fb.geglu_n = 4 * C;
+      ex.conv(fb);
       ex.linear(df, t->ff1.wd, t->ff1.cout, P, C, dl3);
       // norm3 backward inside the cross-attention backward (dl3 = gamma3 dL/dLN3 through the folded weight)
       DCK(dc_crossattn_bwd_ln(r1.p, r1.ld, P, C, H, t->ln2.gamma, t->tabs, sl2, probs, dl3.p, dl3.ld, r2.p, r2.ld, sl3,

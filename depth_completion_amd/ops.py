@@ -142,7 +142,7 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
               cout: int, kh: int = 3, kw: int = 3, stride: int = 1, pad: int = 1, mode: int = 0, x2=None,
               c1: int = 0, bias=None, rowbias=None, rowbias_ld: int = 0, resid=None, mask=None, act: int = 0,
               y=None, splitk: bool = True, algo: int | None = None, nsplit: int | None = None, geglu: int = 0,
-              y2=None, aux=None, rows=None, gn: GnFuse | None = None, ln: LnFuse | None = None):
+              y2=None, aux=None, rows=None, gn: GnFuse | None = None, ln: LnFuse | None = None, geglu_n: int = 0):
     """The dc_conv_desc of one conv_gemm call, its (algo, split) chosen (tuned table / nearest shape).
     gn: fused GroupNorm statistics (include/dcamd.h dc_gn_fuse; the caller keeps it alive); ln: a LayerNorm of the
     input rows folded in (dc_ln_fuse, ln_fuse below; the caller keeps it alive)."""
@@ -173,6 +173,7 @@ def conv_desc(ctx: Ctx, x, w: torch.Tensor, *, nb: int, hin: int, win: int, cin:
     d.ldy2 = LD(y2)
     d.aux = P(aux)
     d.ldaux = LD(aux)
+    d.geglu_n = geglu_n
     d.ws = ctx.ws.data_ptr() if splitk else None
     d.ws_bytes = ctx.ws_bytes if splitk else 0
     if gn is not None:
@@ -309,13 +310,13 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
 
 def linear(ctx: Ctx, x, w: torch.Tensor, rows: int, cout: int, y, bias=None, resid=None, rowbias=None,
            rowbias_ld: int = 0, act: int = 0, geglu: int = 0, y2=None, aux=None, algo: int | None = None,
-           nsplit: int | None = None, gn: GnFuse | None = None, ln: LnFuse | None = None):
+           nsplit: int | None = None, gn: GnFuse | None = None, ln: LnFuse | None = None, geglu_n: int = 0):
     """y[rows, cout] = x[rows, K] @ w[cout, K]^T (+ bias, + resid); geglu 1 / 2: the fused GEGLU
     epilogues of include/dcamd.h (y2 = h * gelu(gate); aux = interleaved pre-activation); ln: LayerNorm(x) as the
     input (w the folded weight, dc_ln_fuse)."""
     return conv_gemm(ctx, x, w, nb=1, hin=1, win=rows, cin=w.shape[1], hout=1, wout=rows, cout=cout, kh=1, kw=1,
                      stride=1, pad=0, bias=bias, resid=resid, rowbias=rowbias, rowbias_ld=rowbias_ld, act=act, y=y,
-                     geglu=geglu, y2=y2, aux=aux, algo=algo, nsplit=nsplit, gn=gn, ln=ln)
+                     geglu=geglu, y2=y2, aux=aux, algo=algo, nsplit=nsplit, gn=gn, ln=ln, geglu_n=geglu_n)
 
 
 def ln_fuse(lin, stats) -> LnFuse:

@@ -16,7 +16,7 @@ import torch
 from . import ops
 from .config import UNetConfig
 from .ops import BF16, Ctx, Slice
-from .weights import Conv, Linear, LnLinear, Norm, fold_cross_attention, geglu_interleave, round_bf16
+from .weights import Conv, FoldedPair, Linear, LnLinear, Norm, fold_cross_attention, geglu_interleave, round_bf16
 
 
 class ResnetW:
@@ -39,6 +39,13 @@ class ResnetW:
         self.temb_tables: dict = {}
 
 
+def ff_fold_enabled() -> bool:
+    """FF2 and proj_out folded into one two-source linear (include/dcamd.h dc_fold_linear_pair; forward and input-
+    gradient one launch each instead of two); DC_FF_FOLD=0: the two linears, for A/B runs and tests -- the native
+    session always folds."""
+    return os.environ.get("DC_FF_FOLD", "1") != "0"
+
+
 def ln_fuse_enabled() -> bool:
     """LayerNorm norm3 folded into ff.net.0.proj (include/dcamd.h dc_ln_fuse: its statistics from the cross-attention
     kernel that produces its input) and its backward into the cross-attention backward; DC_LN_FUSE=0: the separate
@@ -52,7 +59,6 @@ class TransformerW:
         self.ln_fused = ln_fuse_enabled()
         self.norm = Norm(sd[pre + "norm.weight"], sd[pre + "norm.bias"], dev, 1e-6)
         self.proj_in = Linear(sd[pre + "proj_in.weight"], sd[pre + "proj_in.bias"], dev)
-        self.proj_out = Linear(sd[pre + "proj_out.weight"], sd[pre + "proj_out.bias"], dev)
         b = pre + "transformer_blocks.0."
         self.ln1 = Norm(sd[b + "norm1.weight"], sd[b + "norm1.bias"], dev, 1e-5)
         self.ln2 = Norm(sd[b + "norm2.weight"], sd[b + "norm2.bias"], dev, 1e-5)
@@ -70,8 +76,14 @@ class TransformerW:
                                 sd[b + "norm3.weight"], sd[b + "norm3.bias"], 1e-5, dev)
         else:
             self.ff1 = Linear(sd[b + "ff.net.0.proj.weight"][perm], sd[b + "ff.net.0.proj.bias"][perm], dev)
-        self.ff2 = Linear(sd[b + "ff.net.2.weight"], sd[b + "ff.net.2.bias"], dev)
         self.c = self.proj_in.cout
+        self.ffo = self.ff2 = self.proj_out = None
+        if ff_fold_enabled():   # FF2 + proj_out as one linear over [gg | r2]
+            self.ffo = FoldedPair(sd[b + "ff.net.2.weight"], sd[b + "ff.net.2.bias"], sd[pre + "proj_out.weight"],
+                                  sd[pre + "proj_out.bias"], dev)
+        else:
+            self.ff2 = Linear(sd[b + "ff.net.2.weight"], sd[b + "ff.net.2.bias"], dev)
+            self.proj_out = Linear(sd[pre + "proj_out.weight"], sd[pre + "proj_out.bias"], dev)
 
 
 def timestep_embedding(timesteps: torch.Tensor, dim: int) -> torch.Tensor:
@@ -241,6 +253,13 @@ class UNetPlan:
             self._gn_targets.setdefault(id(x2), []).append((acc, c1, self.groups, cpg, hw))
         return acc
 
+    def _conv_fwd(self, x, w, y, linear=False, **kw):
+        """A forward conv / linear producing y, with the fused GroupNorm statistics of y's consumers (_gnf)."""
+        if linear:
+            rows, cout = kw.pop("rows"), kw.pop("cout")
+            kw = dict(nb=1, hin=1, win=rows, cin=w.shape[1], hout=1, wout=rows, cout=cout, kh=1, kw=1, pad=0, **kw)
+        ops.conv_gemm(self.ctx, x, w, y=y, gn=self._gnf(y), **kw)
+
     def _gnf(self, y):
         """dc_gn_fuse (mode 1) for a conv writing y, or None when no GroupNorm reads y."""
         if not self.fuse_gn:
@@ -295,16 +314,16 @@ class UNetPlan:
 
         def f():
             self._gn_fwd(x, hh * ww, cin, r.norm1, True, acc1, g1, st1, x2=x2, c1=c1)
-            ops.conv_gemm(ctx, g1, r.conv1.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
-                          bias=r.conv1.bias, rowbias=r.temb_table, rowbias_ld=cout, y=h1, gn=self._gnf(h1))
+            self._conv_fwd(g1, r.conv1.wf, h1, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
+                           bias=r.conv1.bias, rowbias=r.temb_table, rowbias_ld=cout)
             self._gn_fwd(h1, hh * ww, cout, r.norm2, True, acc2, g2, st2)
             res = x
             if r.shortcut is not None:
                 ops.conv_gemm(ctx, x, r.shortcut.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
                               kh=1, kw=1, pad=0, x2=x2, c1=c1, bias=r.shortcut.bias, y=sc)
                 res = sc
-            ops.conv_gemm(ctx, g2, r.conv2.wf, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout,
-                          bias=r.conv2.bias, resid=res, y=out, gn=self._gnf(out))
+            self._conv_fwd(g2, r.conv2.wf, out, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout,
+                           bias=r.conv2.bias, resid=res)
 
         self.fwd.append(f)
         self.tape.append(("resnet", dict(r=r, x=x, x2=x2, c1=c1, hw=hw, st1=st1, h1=h1, st2=st2, out=out)))
@@ -337,7 +356,7 @@ class UNetPlan:
         self.saved.append(lnf3)
         f8 = self.buf(P, 8 * C)
         gg = self.buf(P, 4 * C)
-        r3 = self.buf(P, C)
+        r3 = self.buf(P, C) if t.ffo is None else None
         out = self.buf(P, C)
         acc0 = self._gn_consumer(x, C, T)
 
@@ -356,8 +375,12 @@ class UNetPlan:
             else:
                 ops.layernorm(ctx, r2, P, C, t.ln3.gamma, t.ln3.beta, t.ln3.eps, l3, sl3)
                 ops.linear(ctx, l3, t.ff1.wf, P, 8 * C, f8, bias=t.ff1.bias, geglu=1, y2=gg)   # + GEGLU
-            ops.linear(ctx, gg, t.ff2.wf, P, C, r3, bias=t.ff2.bias, resid=r2)
-            ops.linear(ctx, r3, t.proj_out.wf, P, C, out, bias=t.proj_out.bias, resid=x, gn=self._gnf(out))
+            if t.ffo is not None:   # (FF2 + residual) -> proj_out + residual as one linear over [gg | r2]
+                self._conv_fwd(gg, t.ffo.wf, out, linear=True, rows=P, cout=C, bias=t.ffo.bias, resid=x, x2=r2,
+                               c1=4 * C)
+            else:
+                ops.linear(ctx, gg, t.ff2.wf, P, C, r3, bias=t.ff2.bias, resid=r2)
+                self._conv_fwd(r3, t.proj_out.wf, out, linear=True, rows=P, cout=C, bias=t.proj_out.bias, resid=x)
 
         self.fwd.append(f)
         self.tape.append(("transformer", dict(t=t, x=x, hw=hw, st0=st0, p=p, sl1=sl1, qkv=qkv, o=o, lse=lse, r1=r1,
@@ -371,8 +394,8 @@ class UNetPlan:
         out = self.buf(nb * ho * wo, cv.cout)
 
         def f():
-            ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, stride=2,
-                          bias=cv.bias, y=out, gn=self._gnf(out))
+            self._conv_fwd(x, cv.wf, out, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, stride=2,
+                           bias=cv.bias)
 
         self.fwd.append(f)
         self.tape.append(("down", dict(cv=cv, x=x, hw=hw, ohw=(ho, wo), out=out)))
@@ -385,8 +408,8 @@ class UNetPlan:
         out = self.buf(nb * ho * wo, cv.cout)
 
         def f():
-            ops.conv_gemm(ctx, x, cv.wf, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, mode=1,
-                          bias=cv.bias, y=out, gn=self._gnf(out))
+            self._conv_fwd(x, cv.wf, out, nb=nb, hin=hh, win=ww, cin=cv.cin, hout=ho, wout=wo, cout=cv.cout, mode=1,
+                           bias=cv.bias)
 
         self.fwd.append(f)
         self.tape.append(("up", dict(cv=cv, x=x, hw=hw, ohw=ohw, out=out)))
@@ -581,8 +604,11 @@ class UNetPlan:
         acc0, gn0 = self._gn_bwd_fuse(x, T, C, t.norm, False, st0)
 
         def b():
-            ops.linear(ctx, dout, t.proj_out.wd, P, C, dr3)
-            ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, df, geglu=2, aux=f8)   # + GEGLU backward
+            if t.ffo is not None:   # dL/dgg (+ GEGLU backward) and dL/dr2 from one linear
+                ops.linear(ctx, dout, t.ffo.wd, P, 5 * C, df, geglu=2, aux=f8, y2=dr3, geglu_n=4 * C)
+            else:
+                ops.linear(ctx, dout, t.proj_out.wd, P, C, dr3)
+                ops.linear(ctx, dr3, t.ff2.wd, P, 4 * C, df, geglu=2, aux=f8)   # + GEGLU backward
             ops.linear(ctx, df, t.ff1.wd, P, C, dl3)   # (fused: gamma3 * dL/dLN3 through the folded weight)
             if fused:   # norm3 backward inside the cross-attention backward
                 ops.crossattn_bwd_ln(ctx, r1, P, C, H, t.ln2.gamma, t.cross_tabs, sl2, probs, dl3, r2, sl3, dr3, dr1)

@@ -109,6 +109,31 @@ class Norm:
         self.eps = eps
 
 
+class FoldedPair:
+    """FF2 (ff.net.2) and proj_out of a transformer block folded into one two-source linear over [gg | r2]
+    (include/dcamd.h dc_fold_linear_pair): out = gg (Wp W2)^T + r2 Wp^T + (Wp b2 + bp) + x, with wf = [bf16(Wp W2) |
+    Wp] [C][5C] and its input-gradient wd = wf^T [5C][C] (columns < 4C: dL/dgg for the GEGLU backward, the rest
+    dL/dr2).  Computed by the library's host function (shared with the native session)."""
+
+    def __init__(self, w2, b2, wp, bp, device):
+        from . import _lib
+
+        w2 = round_bf16(w2).contiguous()
+        wp = round_bf16(wp).contiguous()
+        c, k2 = w2.shape
+        b2 = b2.float().to(BF16).float().contiguous()
+        bp = bp.float().to(BF16).float().contiguous()
+        wf = torch.empty(c, k2 + c, dtype=BF16)
+        wd = torch.empty(k2 + c, c, dtype=BF16)
+        bias = torch.empty(c, dtype=torch.float32)
+        _lib.call("dc_fold_linear_pair", w2.data_ptr(), b2.data_ptr(), c, k2, wp.data_ptr(), bp.data_ptr(),
+                  wf.data_ptr(), wd.data_ptr(), bias.data_ptr())
+        self.cout, self.k2 = c, k2
+        self.wf = wf.to(device)
+        self.wd = wd.to(device)
+        self.bias = bias.to(device)
+
+
 def fold_cross_attention(sd: dict, pre: str, ctx: torch.Tensor, heads: int):
     """attn2 with a constant 2-token context -> (U [H][C], D [H][C], c0 [C]) in fp32.
 

@@ -83,6 +83,16 @@ typedef struct dc_ln_fuse {
  * w, gamma, beta fp32 (bf16-exact values), bias fp32 or NULL; wf bf16 [cout][k] out; csum, cbias fp32 [cout] out */
 int dc_fold_layernorm(const float* w, int cout, int k, const float* gamma, const float* beta, const float* bias,
                       void* wf, float* csum, float* cbias);
+/* FF2 (ff.net.2: y = x W2^T + b2, W2 [c][k2]) and the proj_out after it (z = y' Wp^T + bp, Wp [c][c], where
+ * y' = y + r is FF2's residual sum) folded into one two-source linear over [x | r]:
+ *   z = x (Wp W2)^T + r Wp^T + (Wp b2 + bp)
+ * (BasicTransformerBlock's last residual and Transformer2DModel.proj_out, marigold_dc.py:460-465 through diffusers;
+ * exact in real arithmetic: y' is not rounded to bf16 and Wp W2 is, the order of roundings changes).  w2, b2, wp, bp
+ * fp32 (bf16-exact values); wf bf16 [c][k2 + c] = [bf16(Wp W2) | Wp] out; wd bf16 [k2 + c][c] = wf^T out (its input
+ * gradient: columns < k2 are dL/dx, the GEGLU backward's input, the rest dL/dr); bias fp32 [c] out.  Products in
+ * double, summed in k order, rows on up to 16 host threads (the same bits on every host). */
+int dc_fold_linear_pair(const float* w2, const float* b2, int c, int k2, const float* wp, const float* bp, void* wf,
+                        void* wd, float* bias);
 /* 1 where the fused statistics pay for a GroupNorm of hw pixels x c channels (forward / backward): not where the
  * single-launch GroupNorm (one block per group, levels 2-3 of the UNet) runs it.  Both hosts plan with it. */
 int dc_gn_fuse_pays(int hw, int c, int groups, int backward);
@@ -134,6 +144,10 @@ typedef struct dc_conv_desc {
   const dc_gn_fuse* gn;
   /* optional LayerNorm of the input rows folded in (dc_ln_fuse above; NULL: none) */
   const dc_ln_fuse* ln;
+  /* GEGLU 2 only: 0 = every column; 0 < geglu_n < cout (a multiple of 256): columns < geglu_n get the GEGLU backward
+   * into y (ldy >= 2 geglu_n), columns >= geglu_n are stored plainly into y2[m][c - geglu_n] -- the input-gradient of
+   * FF2 and proj_out folded into one linear (dc_fold_linear_pair) */
+  int geglu_n;
 } dc_conv_desc;
 
 int dc_conv_num_algos(void);

@@ -234,3 +234,4 @@ def test_fused_rejects_bad_targets(ctx):
         ops.linear(ctx, a, wl, n * t, c, y, gn=ops.gn_fuse_fwd([(acc, 0, G, c // G, 48)]))
     with pytest.raises(_lib.DCError):
         ops.linear(ctx, a, wl, n * t, c, y, gn=ops.gn_fuse_fwd([(acc, 8, G, c // G, t)]))   # coff + cout > C
+

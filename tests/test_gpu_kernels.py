@@ -833,6 +833,49 @@ def test_geglu_epilogues(ctx, algo, nsplit):
     assert rel(df.float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("c,rows,algo,nsplit", [(256, 300, 0, 0), (256, 300, 13, 2), (256, 300, 12, -1),
+                                                 (320, 6912, 0, 0)])
+def test_folded_ff2_proj_out(ctx, c, rows, algo, nsplit):
+    """FF2 + proj_out folded into one linear over [gg | r2] (weights.FoldedPair, dc_fold_linear_pair): the forward
+    (two sources, K = 5C) against the two linears in fp32, and the input-gradient with the GEGLU backward on the first
+    4C columns and plain dL/dr2 on the rest (dc_conv_desc.geglu_n) against the two input-gradient linears."""
+    from depth_completion_amd import ops
+    from depth_completion_amd.weights import FoldedPair
+    k2 = 4 * c
+    w2 = rnd(c, k2, scale=1 / math.sqrt(k2), seed=110).cpu()
+    b2 = rnd(c, scale=0.1, seed=111).cpu()
+    wp = rnd(c, c, scale=1 / math.sqrt(c), seed=112).cpu()
+    bp = rnd(c, scale=0.1, seed=113).cpu()
+    f = FoldedPair(w2, b2, wp, bp, dev)
+    gg = rnd(rows, k2, seed=114).to(torch.bfloat16)
+    r2 = rnd(rows, c, seed=115).to(torch.bfloat16)
+    x = rnd(rows, c, seed=116).to(torch.bfloat16)
+    out = torch.empty(rows, c, dtype=torch.bfloat16, device=dev)
+    ops.conv_gemm(ctx, gg, f.wf, nb=1, hin=1, win=rows, cin=5 * c, hout=1, wout=rows, cout=c, kh=1, kw=1, pad=0,
+                  x2=r2, c1=k2, bias=f.bias, resid=x, y=out, algo=algo or None, nsplit=nsplit or None)
+    torch.cuda.synchronize()
+    w2d, wpd = w2.to(dev).double(), wp.to(dev).double()
+    ref = ((gg.double() @ w2d.t() + b2.to(dev).double() + r2.double()) @ wpd.t()) + bp.to(dev).double() + x.double()
+    assert rel(out, ref) < 1e-2
+    # input-gradient: df (GEGLU backward of dL/dgg) and dL/dr2 from one launch
+    f8 = rnd(rows, 2 * k2, seed=117).to(torch.bfloat16)
+    dout = rnd(rows, c, seed=118).to(torch.bfloat16)
+    df = torch.empty(rows, 2 * k2, dtype=torch.bfloat16, device=dev)
+    dr2 = torch.empty(rows, c, dtype=torch.bfloat16, device=dev)
+    ops.linear(ctx, dout, f.wd, rows, 5 * c, df, geglu=2, aux=f8, y2=dr2, geglu_n=k2, algo=algo or None,
+               nsplit=nsplit or None)
+    df0 = torch.empty_like(df)
+    dgg = (dout.double() @ wpd @ w2d).to(torch.bfloat16)   # the two linears' dL/dgg, rounded as the kernel rounds
+    ops.linear(ctx, dgg.contiguous(), torch.eye(k2, device=dev, dtype=torch.bfloat16), rows, k2, df0, geglu=2, aux=f8)
+    torch.cuda.synchronize()
+    assert rel(dr2, dout.double() @ wpd) < 1e-2
+    assert rel(df, df0) < 2e-2
+    with pytest.raises(Exception):   # geglu_n without the GEGLU backward, or not a multiple of 256
+        ops.linear(ctx, dout, f.wd, rows, 5 * c, df, y2=dr2, geglu_n=k2)
+    with pytest.raises(Exception):
+        ops.linear(ctx, dout, f.wd, rows, 5 * c, df, geglu=2, aux=f8, y2=dr2, geglu_n=k2 - 128)
+
+
 @pytest.mark.parametrize("nbytes,offset", [(1 << 10, 0), (1769472, 0), (5 << 20, 4), (3 * (1 << 20) + 7, 3)])
 def test_memset_in_graph_replays(nbytes, offset):
     """dc_memset_async captured in a hipGraph clears its whole range on every replay, after the buffer has been

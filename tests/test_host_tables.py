@@ -187,3 +187,30 @@ def test_conv_pick_exact_nearest_and_filters():
                                                                       (2, 1))]
     assert pick_variant(tie, (0, 1, 1, 200, 64, 1, 200, 64, 1, 1, False, 64)) == (1, 1)            # tie: first
     assert pick_variant([], base) == (0, 0)
+
+
+@pytest.mark.parametrize("c,k2", [(64, 256), (320, 1280)])
+def test_fold_linear_pair_matches_fp64(c, k2):
+    """dc_fold_linear_pair (FF2 + proj_out folded into one linear over [gg | r2]) against fp64 torch: wf = [Wp W2 | Wp]
+    rounded to bf16, wd = wf^T exactly, bias = Wp b2 + bp; and the folded linear gives the two linears' output."""
+    from depth_completion_amd.weights import FoldedPair
+    g = torch.Generator().manual_seed(5)
+    w2 = (torch.randn(c, k2, generator=g) / k2 ** 0.5).to(torch.bfloat16).float()
+    wp = (torch.randn(c, c, generator=g) / c ** 0.5).to(torch.bfloat16).float()
+    b2 = (torch.randn(c, generator=g) * 0.1).to(torch.bfloat16).float()
+    bp = (torch.randn(c, generator=g) * 0.1).to(torch.bfloat16).float()
+    f = FoldedPair(w2, b2, wp, bp, "cpu")
+    wref = (wp.double() @ w2.double()).to(torch.bfloat16)
+    assert f.wf.shape == (c, k2 + c) and f.wd.shape == (k2 + c, c)
+    # (fp64 sums in another order, and the fold's double -> fp32 -> bf16 rounding: a rare tie rounds one ulp apart)
+    diff = (f.wf[:, :k2] != wref)
+    assert float(diff.float().mean()) < 1e-3
+    torch.testing.assert_close(f.wf[:, :k2].float(), wref.float(), rtol=8e-3, atol=1e-7)
+    assert torch.equal(f.wf[:, k2:], wp.to(torch.bfloat16))
+    assert torch.equal(f.wd, f.wf.t().contiguous())
+    torch.testing.assert_close(f.bias.double(), wp.double() @ b2.double() + bp.double(), rtol=1e-6, atol=1e-6)
+    gg = torch.randn(7, k2, generator=g).double()
+    r2 = torch.randn(7, c, generator=g).double()
+    two = ((gg @ w2.double().t() + b2.double() + r2) @ wp.double().t()) + bp.double()
+    one = torch.cat([gg, r2], 1) @ f.wf.double().t() + f.bias.double()
+    assert float((one - two).norm() / two.norm()) < 1e-2

@@ -20,6 +20,9 @@
 #   stepprof                   per-shape conv time inside the graph-replayed step (tools/step_profile.py)
 #   pmcstep                    FETCH_SIZE / WRITE_SIZE / MFMA-busy passes over that same step (tools/pmc_step.py)
 #   py=<script args>           any repo python script (e.g. py=tools/gemm_one.py --m 6912)
+#   tune=<workloads>           time the shapes missing from the committed table (DC_TUNE_COLD=2), e.g. tune=c2:1,c2:8
+#   usetuned                   use that table (copied over the box's tree copy) for the following steps
+#   c2env=<K>=<V>[,<K>=<V>]    C2 bench line with these environment variables (an A/B arm of an opt-in switch)
 set -e
 tag=${1:?tag}
 shift
@@ -107,6 +110,16 @@ for step in "$@"; do
     py=*)
       # shellcheck disable=SC2086
       timeout -k 10 600 python -u ${step#py=} > "$out/py_$n.txt" 2> "$out/py_$n.err" ;;
+    tune=*)
+      # shellcheck disable=SC2046
+      DC_TUNE_COLD=2 timeout -k 10 900 python -u tools/tune_gemm.py --workloads $(echo "${step#tune=}" | tr , ' ') \
+        --out "$out/tuned_gfx950.json" > "$out/tune.log" 2>&1 ;;
+    usetuned)
+      cp "$out/tuned_gfx950.json" depth_completion_amd/tuned_gfx950.json ;;
+    c2env=*)
+      # shellcheck disable=SC2046
+      env $(echo "${step#c2env=}" | tr , ' ') timeout -k 10 400 python -u bench.py --no-cpu-baseline \
+        > "$out/bench_c2_$n.json" 2> "$out/bench_c2_$n.err" ;;
     *)
       echo "unknown step $step" >&2
       exit 2 ;;

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--out", default="gpurun_out/tuned_gfx950.json")
     ap.add_argument("--fresh", action="store_true", help="ignore the committed table")
     ap.add_argument("--retune-3x3", action="store_true",
-                    help="re-time the stride-1 3x3 shapes with cin % 64 == 0 (the halo-kernel contract) over every "
+                    help="re-time the stride-1 3x3 shapes with cin %% 64 == 0 (the halo-kernel contract) over every "
                          "variant, keep the committed choice of every other shape")
     ap.add_argument("--try", dest="try_algos", type=int, nargs="+",
                     help="re-time every shape of the workloads: its committed choice against these algo ids (all "
