@@ -40,6 +40,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md "Peak BF16/FP16 MFMA")
+PEAK_CLOCK_HZ = 2.4e9    # the peak engine clock that figure assumes (2.5 PFLOP/s = 2.4 GHz x 1024 SIMDs x 1024 FLOP)
 PEAK_HBM_GBS = 8000.0
 METRIC = "dense-depth frames/sec at 768x576, 50 guided steps; 1 & 8 MI355X"
 
@@ -97,6 +98,16 @@ def conv_flops(d) -> float:
     return f
 
 
+def conv_bytes(d) -> float:
+    """Algorithmic HBM bytes of one dc_conv_gemm launch: its input activations, weights, outputs and residual once
+    each (bf16), what a launch must move if nothing were re-read (the floor the PMC traffic is compared with)."""
+    M = d.nrows if d.rows else d.nb * d.hout * d.wout
+    b = 2.0 * (d.nb * d.hin * d.win * d.cin + d.cout * d.kh * d.kw * d.cin + M * d.cout)
+    if d.resid:
+        b += 2.0 * M * d.cout
+    return b
+
+
 def measure_conv_kernel(pipe, st, reps: int = 3):
     """Time of the dominant kernel (dc_conv_gemm) inside one graph-replayed guided step.
 
@@ -104,7 +115,7 @@ def measure_conv_kernel(pipe, st, reps: int = 3):
     dc_conv_gemm launch left out.  Each graph is replayed `reps` times between HIP events on the
     launch stream; the difference is the time the step spends in its conv launches, in the step's
     own order and cache state (no per-launch event packets).  Returns (launches, conv ms per step,
-    algorithmic FLOPs per step, kernel nodes of the whole step).
+    algorithmic FLOPs per step, kernel nodes of the whole step, algorithmic bytes per step).
     """
     import torch
     from depth_completion_amd import ops
@@ -152,7 +163,7 @@ def measure_conv_kernel(pipe, st, reps: int = 3):
     finally:
         st["dec"].set_rows(None)
     flops = sum(conv_flops(d) for d in descs)
-    return n, max(t_all - t_rest, 1e-6), flops, nodes
+    return n, max(t_all - t_rest, 1e-6), flops, nodes, sum(conv_bytes(d) for d in descs)
 
 
 def graph_node_counts(raw_graph: int) -> dict:
@@ -459,7 +470,7 @@ def run_worker(args) -> None:
         del line["frame_roofline"]
     elif rank == 0:
         st = pipe._plans[(B * S, h, w)]
-        n_launch, conv_ms, conv_flops_, nodes = measure_conv_kernel(pipe, st)
+        n_launch, conv_ms, conv_flops_, nodes, conv_bytes_ = measure_conv_kernel(pipe, st)
         avg_ms = conv_ms / max(n_launch, 1)
         achieved = conv_flops_ / (conv_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -467,7 +478,8 @@ def run_worker(args) -> None:
                     "kernel": "dc_conv_gemm = conv_gemm_kernel, implicit-GEMM conv/linear (all instantiations)",
                     "launches_per_step": n_launch, "avg_launch_ms": round(avg_ms, 5),
                     "method": "graph-replayed step minus the same graph without its conv launches (HIP events)",
-                    "algorithmic_gflop_per_step": round(conv_flops_ / 1e9, 1)}
+                    "algorithmic_gflop_per_step": round(conv_flops_ / 1e9, 1),
+                    "algorithmic_bytes_per_step": round(conv_bytes_)}
         pmc = pmc_record(h, w, B * S)
         if pmc is not None:
             t = pmc["traffic_bytes_per_launch"]
@@ -475,8 +487,18 @@ def run_worker(args) -> None:
                             hbm_gbs=round(t / (avg_ms * 1e-3) / 1e9, 1), pmc_source=pmc["_file"])
             if pmc.get("traffic_bytes_per_step") is not None:
                 roofline["traffic_per_step"] = round(pmc["traffic_bytes_per_step"])
-            if pmc.get("mfma_util") is not None:
-                roofline["mfma_util"] = pmc["mfma_util"]
+                # counter bytes over the launches' own operands moved once: the re-fetch factor beyond L2
+                roofline["traffic_over_algorithmic"] = round(pmc["traffic_bytes_per_step"] / conv_bytes_, 2)
+            if pmc.get("mfma_busy_cycles_per_step") is not None:
+                # MFMA-busy cycles of the step's conv family over that family's graph-replayed time at the peak
+                # clock x 1024 SIMDs: one v_mfma_f32_16x16x32_bf16 (16 K FLOP) keeps a SIMD busy 16 cycles, so this
+                # is >= frac by construction (it counts padding and split-hi/lo MFMAs that frac does not)
+                roofline["mfma_util"] = round(pmc["mfma_busy_cycles_per_step"] /
+                                              (conv_ms * 1e-3 * PEAK_CLOCK_HZ * 1024), 4)
+                roofline["mfma_util_def"] = ("PMC SQ_VALU_MFMA_BUSY_CYCLES per step / (graph-timed family ms x "
+                                             "2.4 GHz x 1024 SIMDs)")
+            if pmc.get("mfma_util_pmc_window") is not None:
+                roofline["mfma_util_pmc_window"] = round(pmc["mfma_util_pmc_window"], 4)
         line["roofline"] = roofline
         line["launches"] = {"kernel_nodes_per_guided_step": nodes.get("kernel"), "graph_nodes": nodes}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not dry:

@@ -66,10 +66,15 @@ def main():
         "traffic_bytes_per_launch": (fetch_b + write_b) / max(n_calls, 1),
         "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE as is; KiB -> bytes",
         "latent_shape": [1, 72, 96],
-        "mfma_util": (m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
-                      if m["GRBM_GUI_ACTIVE"] else None),
-        "mfma_util_def": "sum SQ_VALU_MFMA_BUSY_CYCLES / (sum GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) over the family's "
-                         "dispatches of the step",
+        "mfma_busy_cycles_per_step": m["SQ_VALU_MFMA_BUSY_CYCLES"],
+        "grbm_gui_active_per_step": m["GRBM_GUI_ACTIVE"],
+        # over the profiler's serialised dispatch windows (each dispatch's GRBM_GUI_ACTIVE includes its own ramp and
+        # drain), so it reads below the graph-timed utilisation; bench.py normalises the busy cycles by the
+        # graph-replayed family time instead (roofline.mfma_util)
+        "mfma_util_pmc_window": (m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
+                                 if m["GRBM_GUI_ACTIVE"] else None),
+        "mfma_util_pmc_window_def": "sum SQ_VALU_MFMA_BUSY_CYCLES / (sum GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) over the "
+                                    "family's dispatches of the step, each dispatch serialised by the profiler",
     }
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
