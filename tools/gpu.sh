@@ -21,6 +21,7 @@
 #   pmcstep                    FETCH_SIZE / WRITE_SIZE / MFMA-busy passes over that same step (tools/pmc_step.py)
 #   py=<script args>           any repo python script (e.g. py=tools/gemm_one.py --m 6912)
 #   tune=<workloads>           time the shapes missing from the committed table (DC_TUNE_COLD=2), e.g. tune=c2:1,c2:8
+#   tunefresh=<workloads>      the same over every shape of the workloads (--fresh: the committed table ignored)
 #   usetuned                   use that table (copied over the box's tree copy) for the following steps
 #   c2env=<K>=<V>[,<K>=<V>]    C2 bench line with these environment variables (an A/B arm of an opt-in switch)
 set -e
@@ -113,6 +114,10 @@ for step in "$@"; do
     tune=*)
       # shellcheck disable=SC2046
       DC_TUNE_COLD=2 timeout -k 10 900 python -u tools/tune_gemm.py --workloads $(echo "${step#tune=}" | tr , ' ') \
+        --out "$out/tuned_gfx950.json" > "$out/tune.log" 2>&1 ;;
+    tunefresh=*)
+      # shellcheck disable=SC2046
+      DC_TUNE_COLD=2 timeout -k 10 1100 python -u tools/tune_gemm.py --fresh --workloads $(echo "${step#tunefresh=}" | tr , ' ') \
         --out "$out/tuned_gfx950.json" > "$out/tune.log" 2>&1 ;;
     usetuned)
       cp "$out/tuned_gfx950.json" depth_completion_amd/tuned_gfx950.json ;;

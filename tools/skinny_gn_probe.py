@@ -1,6 +1,7 @@
 """Probe (GPU, timing only): the level-2 / level-3 skinny convs with and without the fused GroupNorm statistics
 (dc_gn_fuse modes 1 / 2) in their epilogues, and the diagnostic arms that skip parts of it (DC_HALO_DIAG 8: no
-accumulator adds), each call timed inside a 20-call graph.  Args: none."""
+accumulator adds; 16: no block fold either), each call timed inside a 20-call graph.
+Args: [skinny | halo] (the level-2 / 3 skinny shapes, or level-0 / 1 halo shapes)."""
 import math
 import os
 import sys
@@ -42,8 +43,10 @@ def r(*s):
     return (torch.randn(*s, device=dev) * 0.05).to(torch.bfloat16)
 
 
-for h, w, c, algo, ns in [(9, 12, 1280, 43, -10), (9, 12, 1280, 43, 10), (9, 12, 1280, 43, 1), (18, 24, 1280, 47, -4),
-                          (18, 24, 640, 47, -4)]:
+SHAPES = {"skinny": [(9, 12, 1280, 43, -10), (9, 12, 1280, 43, 10), (9, 12, 1280, 43, 1), (18, 24, 1280, 47, -4),
+                     (18, 24, 640, 47, -4)],
+          "halo": [(72, 96, 320, 33, 1), (36, 48, 640, 31, 3), (36, 48, 640, 33, 1), (72, 96, 640, 62, 1)]}
+for h, w, c, algo, ns in SHAPES[sys.argv[1] if len(sys.argv) > 1 else "skinny"]:
     x = r(h * w, c)
     wt = pack_conv(torch.randn(c, c, 3, 3) / math.sqrt(9 * c)).to(dev, torch.bfloat16)
     res = r(h * w, c)
@@ -56,8 +59,8 @@ for h, w, c, algo, ns in [(9, 12, 1280, 43, -10), (9, 12, 1280, 43, 10), (9, 12,
     g1 = ops.gn_fuse_fwd([(acc, 0, G, c // G, h * w)])
     g2 = ops.gn_fuse_bwd(acc, G, c // G, h * w, x, st, gam, bet, True)
     out = []
-    for name, gn, diag in [("plain", None, "0"), ("gn1", g1, "0"), ("gn1 no-adds", g1, "8"), ("gn2", g2, "0"),
-                           ("gn2 no-adds", g2, "8")]:
+    for name, gn, diag in [("plain", None, "0"), ("gn1", g1, "0"), ("gn1 no-adds", g1, "8"),
+                           ("gn1 no-fold", g1, "16"), ("gn2", g2, "0"), ("gn2 no-adds", g2, "8")]:
         os.environ["DC_HALO_DIAG"] = diag
         out.append(f"{name} {graph_time(lambda: ops.conv_gemm(ctx, x, wt, y=y, gn=gn, **kw)):.1f}")
     os.environ["DC_HALO_DIAG"] = "0"
