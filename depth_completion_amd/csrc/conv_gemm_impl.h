@@ -383,34 +383,67 @@ __device__ __forceinline__ void gn_epilogue_rows(const ConvGemmParams& p, char* 
   }
   bf16x8 keep[RMAX];
   long mrow[RMAX];
+  // the global operands of the lane's rows in one batch ahead of the staging reads and the arithmetic (the row bias,
+  // residual and -- backward -- the GroupNorm input x and the frame's (mean, rstd)); loaded per row where they are
+  // used, each was a dependent memory round trip behind the staging reads or the frame test
+  bf16x8 rres[RMAX], rx[GNM == 2 ? RMAX : 1], rbias;
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) {
     const int g = lane + 64 * r;
-    const int row = g / GPR;
-    mrow[r] = (g < WM * GPR && cok) ? pix_of(row) : -1;
+    mrow[r] = (g < WM * GPR && cok) ? pix_of(g / GPR) : -1;
+    const long m = mrow[r];
+    if (m < 0) continue;
+    if (p.resid) rres[r] = *reinterpret_cast<const bf16x8*>(p.resid + m * p.ldr + c);
+    if constexpr (GNM == 2)
+      rx[r] = c < G.c1 ? *reinterpret_cast<const bf16x8*>(G.x + m * G.ldx + c)
+                       : *reinterpret_cast<const bf16x8*>(G.x2 + m * G.ldx2 + (c - G.c1));
+  }
+  if (p.rowbias && cok) rbias = *reinterpret_cast<const bf16x8*>(p.rowbias + (long)(*p.rowbias_idx) * p.rowbias_ld + c);
+  auto load_stats = [&](int f) {
+    const float* st = G.stats + (long)f * t0.groups * 2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int gi = (c + i) / t0.cpg;
+      mu[i] = st[gi * 2];
+      rs[i] = st[gi * 2 + 1];
+    }
+    fcur = f;
+  };
+  if (GNM == 2 && uni && cok) load_stats(fa);
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) {
+    const int row = (lane + 64 * r) / GPR;
     const long m = mrow[r];
     if (m < 0) continue;
     float v[8];
     load8(es + row * lde + cg * 8, v);
-    epilogue_values8(p, m, c, v);
+    // epilogue_values8 with the preloaded operands
+    if (p.rowbias) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (float)(bf16)v[i] + (float)rbias[i];
+    }
+    if (p.resid) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (float)(bf16)v[i] + (float)rres[r][i];
+    }
+    if (p.act == 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = fmaxf(v[i], 0.0f);
+    }
+    if (p.mask) {
+      float mf[8];
+      load8(p.mask + m * p.ldmask + c, mf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = mf[i] > 0.0f ? v[i] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)(bf16)v[i];
     const int f = uni ? fa : (int)fast_div((unsigned)m, t0.hw_mul, t0.hw_shr);
     if constexpr (GNM == 2) {
-      if (f != fcur) {
-        const float* st = G.stats + (long)f * t0.groups * 2;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int gi = (c + i) / t0.cpg;
-          mu[i] = st[gi * 2];
-          rs[i] = st[gi * 2 + 1];
-        }
-        fcur = f;
-      }
-      float xf[8];
-      if (c < G.c1) load8(G.x + m * G.ldx + c, xf);
-      else load8(G.x2 + m * G.ldx2 + (c - G.c1), xf);
+      if (f != fcur) load_stats(f);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float xh = (xf[i] - mu[i]) * rs[i];
+        const float xh = ((float)rx[r][i] - mu[i]) * rs[i];
         float dd = v[i];
         if (G.silu) {
           const float yv = (float)(bf16)(xh * ga[i] + be[i]);
