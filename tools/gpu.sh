@@ -24,6 +24,7 @@
 #   tunefresh=<workloads>      the same over every shape of the workloads (--fresh: the committed table ignored)
 #   usetuned                   use that table (copied over the box's tree copy) for the following steps
 #   c2env=<K>=<V>[,<K>=<V>]    C2 bench line with these environment variables (an A/B arm of an opt-in switch)
+#   c3env=<K>=<V>[,<K>=<V>]    the same for C3 (batch 8)
 set -e
 tag=${1:?tag}
 shift
@@ -125,6 +126,10 @@ for step in "$@"; do
       # shellcheck disable=SC2046
       env $(echo "${step#c2env=}" | tr , ' ') timeout -k 10 400 python -u bench.py --no-cpu-baseline \
         > "$out/bench_c2_$n.json" 2> "$out/bench_c2_$n.err" ;;
+    c3env=*)
+      # shellcheck disable=SC2046
+      env $(echo "${step#c3env=}" | tr , ' ') timeout -k 10 400 python -u bench.py --batch 8 --steps 2 --warmup 1 \
+        --no-cpu-baseline > "$out/bench_c3_$n.json" 2> "$out/bench_c3_$n.err" ;;
     *)
       echo "unknown step $step" >&2
       exit 2 ;;
