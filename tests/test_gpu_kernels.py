@@ -321,7 +321,7 @@ def test_layernorm_fwd_bwd(ctx, c):
 
 @pytest.mark.parametrize("c,n,geglu", [(320, 960, 0), (640, 1920, 0), (1280, 3840, 0), (320, 2560, 1),
                                         (1280, 10240, 1)])
-@pytest.mark.parametrize("algo,nsplit", [(13, 1), (12, 1), (3, 1), (37, 1), (18, 1), (13, 3), (12, -1)])
+@pytest.mark.parametrize("algo,nsplit", [(13, 1), (12, 1), (3, 1), (37, 1), (18, 1), (13, 3), (12, -1), (11, 1), (14, 1)])
 def test_linear_ln_fused(ctx, c, n, geglu, algo, nsplit):
     """LayerNorm folded into the consuming linear (dc_ln_fuse: the rows' (mean, rstd) given, the normalisation
     applied in the epilogue after split-K / stream-K sums) against torch: bf16(LayerNorm(x)) @ W^T + bias in fp32.
