@@ -12,6 +12,7 @@
 #   c2 | c2cpu                 C2 bench line (c2cpu: with the CPU baseline)
 #   c2at=<dir>                 C2 bench line of the tree copy in <dir> (A/B arm)
 #   c3 | c4 | c4b8 | c5        C3 batch 8, C4 KITTI 64-beam (batch 1 / 8), C5 10-seed ensemble bench lines
+#   c4at=<dir> | c5at=<dir>    the C4 / C5 bench line of the tree copy in <dir> (A/B arm)
 #   trace                      rocprofv3 --kernel-trace --stats of a short C2 bench
 #   trace3                     the same for C3 (batch 8)
 #   calltrace                  kernel trace of 4 C2 calls, itemised outside the step graphs (tools/call_timeline.py)
@@ -54,6 +55,14 @@ for step in "$@"; do
       # the C2 bench line of another tree (an A/B arm: a full copy of a tree with its built library, e.g. ab/old)
       d=${step#c2at=}
       (cd "$d" && timeout -k 10 400 python -u bench.py --no-cpu-baseline) > "$out/bench_c2_$n.json" 2> "$out/bench_c2_$n.err" ;;
+    c4at=*)
+      d=${step#c4at=}
+      (cd "$d" && timeout -k 10 300 python -u bench.py --height 352 --width 1216 --pattern beams --no-cpu-baseline) \
+        > "$out/bench_c4_$n.json" 2> "$out/bench_c4_$n.err" ;;
+    c5at=*)
+      d=${step#c5at=}
+      (cd "$d" && timeout -k 10 400 python -u bench.py --height 900 --width 1600 --points 3000 --seeds 10 --steps 2 \
+        --warmup 1 --no-cpu-baseline) > "$out/bench_c5_$n.json" 2> "$out/bench_c5_$n.err" ;;
     c2cpu)
       timeout -k 10 600 python -u bench.py > "$out/bench_c2.json" 2> "$out/bench_c2.err" ;;
     c3)
@@ -61,13 +70,15 @@ for step in "$@"; do
         > "$out/bench_c3_b8.json" 2> "$out/bench_c3_b8.err" ;;
     c4)
       timeout -k 10 300 python -u bench.py --height 352 --width 1216 --pattern beams --no-cpu-baseline \
-        > "$out/bench_c4.json" 2> "$out/bench_c4.err" ;;
+        > "$out/bench_c4.json" 2> "$out/bench_c4.err"
+      cp "$out/bench_c4.json" "$out/bench_c4_$n.json" ;;
     c4b8)
       timeout -k 10 300 python -u bench.py --height 352 --width 1216 --pattern beams --batch 8 --steps 2 --warmup 1 \
         --no-cpu-baseline > "$out/bench_c4_b8.json" 2> "$out/bench_c4_b8.err" ;;
     c5)
       timeout -k 10 400 python -u bench.py --height 900 --width 1600 --points 3000 --seeds 10 --steps 2 --warmup 1 \
-        --no-cpu-baseline > "$out/bench_c5.json" 2> "$out/bench_c5.err" ;;
+        --no-cpu-baseline > "$out/bench_c5.json" 2> "$out/bench_c5.err"
+      cp "$out/bench_c5.json" "$out/bench_c5_$n.json" ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- \
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$out/trace_bench.json" 2> "$out/trace.err" ;;
