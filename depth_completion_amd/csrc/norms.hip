@@ -416,6 +416,8 @@ __global__ void gn_bwd_apply_kernel(GNShape s, const float* stats, const float* 
 // owns a contiguous range of groups (its L2 holds its own channel slice of each row).
 template <int VEC>
 using bfvec = __bf16 __attribute__((ext_vector_type(VEC)));
+template <int VEC>
+using fvec = float __attribute__((ext_vector_type(VEC)));
 
 constexpr int kGroupThreads = 1024;
 constexpr int kGroupRed = 32 * sizeof(double);          // reduction scratch in front of the stash
@@ -534,7 +536,10 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double* red = reinterpret_cast<double*>(smem);
   bfvec<VEC>* sx = reinterpret_cast<bfvec<VEC>*>(smem + kGroupRed);
-  bfvec<VEC>* sd = sx + (long)s.hw * vpr;
+  // pass 1 keeps g dy' (fp32) next to x, so pass 2 does not recompute the SiLU gradient (an exact-division sigmoid
+  // per element, the kernel's VALU bulk on the one CU that owns the group)
+  fvec<VEC>* sg = reinterpret_cast<fvec<VEC>*>(
+      smem + ((kGroupRed + (long)s.hw * vpr * VEC * 2 + 31) & ~31L));   // (32-B aligned: the host adds 32 bytes)
   const int L = gn_group_block(s.nb * s.groups);
   const int n = L / s.groups, g = L % s.groups;
   const int v = threadIdx.x % vpr, r0 = threadIdx.x / vpr;
@@ -591,14 +596,16 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
         const int row = r + u * RP;
         if (row >= s.hw) continue;
         sx[row * vpr + v] = rx[u];
-        sd[row * vpr + v] = rd[u];
+        fvec<VEC> gv;
 #pragma unroll
         for (int i = 0; i < VEC; ++i) {
           float xh;
           const float gd = elem((float)rx[u][i], (float)rd[u][i], i, xh);
+          gv[i] = gd;
           sa += gd;
           sb += gd * xh;
         }
+        sg[row * vpr + v] = gv;
       }
     }
   }
@@ -609,13 +616,13 @@ __global__ __launch_bounds__(kGroupThreads) void gn_group_bwd_kernel(GNShape s, 
   if (!act) return;
   bf16* dst = dx + (long)n * s.hw * lddx + ch;
   for (int row = r0, j = 0; row < s.hw; row += RP, ++j) {
-    const bfvec<VEC> rx = sx[row * vpr + v], rd = sd[row * vpr + v];
+    const bfvec<VEC> rx = sx[row * vpr + v];
+    const fvec<VEC> gv = sg[row * vpr + v];
     float out[VEC];
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
-      float xh;
-      const float gd = elem((float)rx[i], (float)rd[i], i, xh);
-      out[i] = rs * (gd - ma - xh * mb);
+      const float xh = ((float)rx[i] - mu) * rs;   // as elem() forms it
+      out[i] = rs * (gv[i] - ma - xh * mb);
     }
     if (add1) {
       bfvec<VEC> e;
@@ -711,7 +718,7 @@ int gn_group_vec(const GNShape& s, int tensors, long cap, std::initializer_list<
     cap = v < 0 ? kGroupLds : v;
   }
   const long slice = (long)s.hw * s.cpg * 2;
-  if (slice > cap || tensors * slice + kGroupRed > kGroupLds) return 0;
+  if (slice > cap || tensors * slice + kGroupRed + 32 > kGroupLds) return 0;
   for (int vec = 8; vec >= 2; vec >>= 1) {
     if (s.cpg % vec || s.cpg / vec > kGroupThreads) continue;
     bool ok = true;
@@ -784,10 +791,11 @@ extern "C" int dc_groupnorm_bwd(const void* x, int ldx, const void* x2, int ldx2
   if (!gn_make_shape(s, x, ldx, x2, ldx2, c1, nb, hw, c, groups) || !dy || !dx || !stats || !ws) return DC_ERR_ARG;
   if (lddy % 8 || lddx % 8 || (add1 && ldadd1 % 8) || (add2 && ldadd2 % 8)) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
-  if (const int vec = gn_group_vec(s, 2, kGroupCapBwd, {s.x, s.x2, dy, dx, add1 ? add1 : dx, add2 ? add2 : dx})) {
+  // (the stash: x in bf16 and g dy' in fp32, three slices' worth)
+  if (const int vec = gn_group_vec(s, 3, kGroupCapBwd, {s.x, s.x2, dy, dx, add1 ? add1 : dx, add2 ? add2 : dx})) {
     const int vpr = s.cpg / vec, RP = kGroupThreads / vpr;
     const dim3 grid(nb * groups), blk(kGroupThreads);
-    const size_t lds = kGroupRed + 2 * (size_t)hw * s.cpg * 2;
+    const size_t lds = kGroupRed + 3 * (size_t)hw * s.cpg * 2 + 32;
 #define DC_GN_GROUP_BWD(V, U)                                                                                   \
   DC_GN_GROUP_LAUNCH((gn_group_bwd_kernel<V, U>), s, vpr, RP, stats, gamma, beta, silu, (const bf16*)dy, lddy,  \
                      (bf16*)dx, lddx, (const bf16*)add1, ldadd1, (const bf16*)add2, ldadd2)
@@ -824,7 +832,7 @@ extern "C" int dc_gn_fuse_pays(int hw, int c, int groups, int backward) {
   GNShape s;
   alignas(16) static const bf16 dummy[8] = {};
   if (!gn_make_shape(s, dummy, c, nullptr, 0, 0, 1, hw, c, groups)) return 0;
-  return gn_group_vec(s, backward ? 2 : 1, backward ? kGroupCapBwd : kGroupCapFwd, {dummy}) ? 0 : 1;
+  return gn_group_vec(s, backward ? 3 : 1, backward ? kGroupCapBwd : kGroupCapFwd, {dummy}) ? 0 : 1;
 }
 
 extern "C" long long dc_gn_acc_bytes(int nb, int groups) {
