@@ -16,8 +16,10 @@ Also reported on the JSON line:
   roofline       the dominant kernel (implicit-GEMM conv/linear, dc_conv_gemm): the time a graph-replayed
                  guided step spends in its conv launches (HIP events on the launch stream: the step's graph
                  minus the same graph without them), algorithmic FLOPs / that time; `traffic` / `hbm_gbs`
-                 / `mfma_util` from the committed PMC passes (profiles/pmc_conv_gemm*.json, gfx950
-                 corrections of MI355X_MICROARCH.md) for the latent shape they ran on
+                 from the committed PMC passes over the graph-replayed step (profiles/pmc_step*.json, gfx950
+                 corrections of MI355X_MICROARCH.md) for the latent shape they ran on;
+                 `traffic_over_algorithmic` = those bytes over the launches' operands moved once (conv_bytes);
+                 `mfma_util` = the PMC MFMA-busy cycles over the graph-timed family time x 2.4 GHz x 1024 SIMDs
   frame_roofline algorithmic TFLOP per frame (depth_completion_amd/flops.py, SURVEY §8d convention, at the
                  run's own latent shape, steps and seeds) x fps / 2.5 PF
   launches       kernel nodes of one captured guided step (hipGraphGetNodes)
