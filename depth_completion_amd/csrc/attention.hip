@@ -1031,6 +1031,10 @@ int attn_cfg(int t, int heads, int nb, bool bwd) {
   const int forced = e ? atoi(e) : -1;
   const int ncfg = bwd ? kNumBwdCfgs : kNumAttnCfgs;
   if (forced >= 0 && forced < (bwd ? kNumBwdCfgs + 1 : kNumAttnCfgs)) return forced;
+  // short sequences (levels 2-3 at batch 1: T = 432 / 108, 20 heads): the backward's (2, 2) blocks -- twice the
+  // blocks of (4, 2) over the same key tiles -- measured 22.1 vs 26.2 us at T = 432 (profiles/r05aa/); the model
+  // below does not see it (it prices resident waves, not the sequential key-tile chain of a small grid)
+  if (bwd && (long)t * nb <= 512) return 2;
   int best = 0;
   double best_t = 1e30;
   for (int i = 0; i < ncfg; ++i) {

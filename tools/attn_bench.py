@@ -33,7 +33,7 @@ def timed(fn, n=10):
     return e0.elapsed_time(e1) / n
 
 
-for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (8, 6912, 5), (8, 1728, 10)]:
+for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (1, 108, 20), (8, 6912, 5), (8, 1728, 10), (8, 432, 20)]:
     C = heads * 64
     qkv = (torch.randn(n * t, 3 * C, device=dev)).to(torch.bfloat16)
     o = torch.empty(n * t, C, dtype=torch.bfloat16, device=dev)
