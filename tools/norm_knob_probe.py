@@ -1,7 +1,8 @@
 """Probe (GPU, timing only): LayerNorm fwd / bwd and the one-pass GroupNorm apply (fused-statistics form) at the
 UNet's shapes under the launch-shape knobs DC_LN_WPB (waves per LayerNorm block), DC_GN_T (threads per GroupNorm
 apply block, rounded to whole 8-channel rows) and DC_GN_BPF (GroupNorm apply blocks per frame); each call timed
-inside a 20-call graph captured under the setting.  Args: none."""
+inside a 20-call graph captured under the setting.  The knobs existed in norms.hip only for this probe (round 5,
+profiles/r05ac/: the committed shapes won); without them every setting times the committed shape.  Args: none."""
 import os
 import sys
 
