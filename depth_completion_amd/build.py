@@ -16,7 +16,8 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libdcamd.so"
 OBJ_DIR = PKG / "build_obj"
-SOURCES = ["conv_gemm.hip", "conv_skinny9.hip", "conv_skinny1.hip", "conv_gemm_gn.hip", "conv_gemm_gnb.hip", "conv_gemm_ln.hip", "norms.hip", "attention.hip", "crossattn.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
+SOURCES = ["conv_gemm.hip", "conv_skinny9.hip", "conv_skinny1.hip", "conv_skinny9_gn.hip", "conv_skinny9_gnb.hip",
+           "conv_skinny1_gn.hip", "conv_skinny1_gnb.hip", "conv_gemm_gn.hip", "conv_gemm_gnb.hip", "conv_gemm_ln.hip", "norms.hip", "attention.hip", "crossattn.hip", "elementwise.hip", "guidance.hip", "metrics.hip", "vae_kl.hip",
            "rowsets.hip", "ensemble.hip", "host_tables.cpp", "session.cpp", "version.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DC_OFFLOAD_ARCH", "gfx950")

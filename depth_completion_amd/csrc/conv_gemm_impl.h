@@ -525,6 +525,133 @@ __device__ __forceinline__ void gn_epilogue_rows(const ConvGemmParams& p, char* 
     if (mrow[r] >= 0) *reinterpret_cast<bf16x8*>(p.y + mrow[r] * p.ldy + c) = keep[r];
 }
 
+// ---- fused GroupNorm statistics for the block-staged epilogues (the skinny kernels and their split-K reduce kernel):
+// the block's store loop visits (row, 8-channel column group) pairs g = tid, tid + 256, ... so a thread keeps one
+// column group (GPR = BN / 8 divides 256).  add() takes a row's final values (epilogue_values8) and, for GNM 2, turns
+// them into dy' (stored in their place) as gn_epilogue_rows does; the running sums belong to one frame and are added
+// per thread when the frame changes (row runs across frames: batched linears).  finish(): a block whose rows lie in
+// one frame folds its threads' sums in LDS (fixed order) and adds once per group; otherwise each thread adds its own.
+template <int GNM, int GPR>
+struct GnTileSums {
+  float s[8], q[8];
+  float ga[8], be[8], mu[8], rs[8];
+  int fcur;   // frame of the running sums (-1: none yet)
+  int fst;    // frame of the loaded (mean, rstd) (GNM 2)
+  int c;      // the thread's first channel (-1: no column group in range)
+
+  __device__ __forceinline__ void init(const ConvGemmParams& p, int c0) {
+    c = c0 < p.cout ? c0 : -1;
+    fcur = fst = -1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = q[i] = 0.0f;
+    if (GNM == 2 && c >= 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        ga[i] = p.gn.gamma[c + i];
+        be[i] = p.gn.beta[c + i];
+      }
+    }
+  }
+  __device__ __forceinline__ void flush(const ConvGemmParams& p) {
+    if (fcur < 0) return;
+    if (!(p.diag & 8))
+      for (int k = 0; k < p.gn.nt; ++k) gn_add_channels(p.gn.t[k], fcur, c, s, q);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = q[i] = 0.0f;
+    fcur = -1;
+  }
+  // row m (frame f) of the thread's column group: v = the stored values on return
+  __device__ __forceinline__ void add(const ConvGemmParams& p, long m, int f, float* v) {
+    if (f != fcur) {
+      flush(p);
+      fcur = f;
+    }
+    if constexpr (GNM == 2) {
+      const GnFuseP& G = p.gn;
+      if (f != fst) {
+        const float* st = G.stats + (long)f * G.t[0].groups * 2;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int gi = (c + i) / G.t[0].cpg;
+          mu[i] = st[gi * 2];
+          rs[i] = st[gi * 2 + 1];
+        }
+        fst = f;
+      }
+      float xf[8];
+      if (c < G.c1) load8(G.x + m * G.ldx + c, xf);
+      else load8(G.x2 + m * G.ldx2 + (c - G.c1), xf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float xh = (xf[i] - mu[i]) * rs[i];
+        float dd = v[i];
+        if (G.silu) {
+          const float yv = (float)(bf16)(xh * ga[i] + be[i]);
+          dd = (float)(bf16)(dd * silu_grad(yv));
+        }
+        const float gd = dd * ga[i];
+        s[i] += gd;
+        q[i] += gd * xh;
+        v[i] = dd;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s[i] += v[i];
+        q[i] += v[i] * v[i];
+      }
+    }
+  }
+  // every thread of the block; uni: all the block's rows are in frame fa.  red: >= (256 * 16 + 2 * BN) floats of LDS
+  // that no thread reads any more (the barrier first)
+  template <int BN>
+  __device__ __forceinline__ void finish(const ConvGemmParams& p, float* red, int n0, bool uni, int fa) {
+    if (!uni) {
+      if (c >= 0) flush(p);
+      return;
+    }
+    const int tid = threadIdx.x;
+    float* col = red + 256 * 16;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[tid * 16 + i] = s[i];
+      red[tid * 16 + 8 + i] = q[i];
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int ccg = tid >> 3, ci = tid & 7;
+      float a = 0.0f, b = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 256 / GPR; ++j) {
+        a += red[(ccg + GPR * j) * 16 + ci];
+        b += red[(ccg + GPR * j) * 16 + 8 + ci];
+      }
+      col[tid] = a;
+      col[BN + tid] = b;
+    }
+    __syncthreads();
+    if (p.diag & 8) return;
+    const int cend = min(n0 + BN, p.cout);
+    for (int k = 0; k < p.gn.nt; ++k) {
+      const GnTargetP& t = p.gn.t[k];
+      const int g = (n0 + t.coff) / t.cpg + tid;
+      const int lo = max(g * t.cpg - t.coff, n0), hi = min((g + 1) * t.cpg - t.coff, cend);
+      if (lo < hi) {
+        float a = 0.0f, b = 0.0f;
+        for (int ch = lo; ch < hi; ++ch) {
+          a += col[ch - n0];
+          b += col[BN + ch - n0];
+        }
+        unsigned long long* w = t.acc + ((blockIdx.x + blockIdx.y) & (kGnReplicas - 1)) * t.rstride +
+                                ((long)fa * t.groups + g) * kGnPair;
+        gn_acc_add(w, a);
+        gn_acc_add(w + kGnWords, b);
+      }
+    }
+  }
+};
+
 // -DDC_DEBUG_LDS (debug builds only, tools/debug_lds.sh): every LDS-DMA wave-instruction's 1 KiB destination and
 // every epilogue staging row is asserted inside the block's static LDS allocation
 #ifdef DC_DEBUG_LDS

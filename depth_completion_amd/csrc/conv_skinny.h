@@ -1,7 +1,8 @@
 #pragma once
 // Weight-streaming "skinny" conv / linear for the few-pixel layers of a batch-1 step (included after conv_gemm_impl.h,
 // inside an anonymous namespace, by conv_gemm.hip for the variant table / contract and by conv_skinny9.hip /
-// conv_skinny1.hip for the kernels; dc_conv_gemm algo ids after the halo and im2col variants).
+// conv_skinny1.hip (and their fused-GroupNorm-statistics forms, conv_skinny{9,1}_gn.hip) for the kernels;
+// dc_conv_gemm algo ids after the halo and im2col variants).
 //
 // UNet levels 2-3 at batch 1 have M = 432 / 108 output pixels against 1280-2560 channels: a 3x3 conv there reads
 // 29.5 MB of weights for 3-13 GFLOP, so the launch is bound by how fast the weights stream from HBM (and, at
@@ -23,8 +24,9 @@
 // last-arriving block (splitk > 0) or by a second kernel over (tile, fragment row) (splitk < 0); the epilogue stages
 // the tile in LDS and writes 16-B rows.
 // Contract (skinny_eligible): KT 9 = the halo contract (3x3, stride 1, pad 1, direct or nearest-upsample input,
-// whole 64-channel chunks); KT 1 = 1x1 / linear over whole 64-channel chunks; no row list, no GEGLU, no fused
-// GroupNorm statistics; input chunks a multiple of U.
+// whole 64-channel chunks); KT 1 = 1x1 / linear over whole 64-channel chunks; no row list, no GEGLU; input chunks a
+// multiple of U.  Fused GroupNorm statistics (dc_gn_fuse modes 1 / 2) ride in the epilogue that stores the tile: the
+// unsplit / last-arriving block's, or skinny_reduce_kernel's.
 
 template <int KT, int TH, int TW, int NJ, int U>
 struct SkinnyCfg {
@@ -48,7 +50,7 @@ struct SkinnyCfg {
   static_assert(KT == 1 || W8 * 128 * 2 + 2 * 128 < 65536, "tap offsets as ds_read immediates");
 };
 
-template <int KT, int TH, int TW, int NJ, int U>
+template <int KT, int TH, int TW, int NJ, int U, int GNM>
 struct SkinnyBlock {
   using C = SkinnyCfg<KT, TH, TW, NJ, U>;
   static constexpr int MI = C::MI, G = C::G, LA = C::LA, NA = C::NA;
@@ -335,6 +337,7 @@ struct SkinnyBlock {
   }
 
   // ---- epilogue: bias in fp32, the block's tile staged as bf16 in LDS, then 16-B rows of BN channels per pixel
+  // (GNM: with the fused GroupNorm statistics of the stored rows, GnTileSums)
   __device__ __forceinline__ void epilogue(int wid, long M) {
     const int col_l = lane & 15, row_l = (lane >> 4) * 4;
     __syncthreads();
@@ -352,6 +355,8 @@ struct SkinnyBlock {
     __syncthreads();
     if (p.diag & 64) return;   // experiments only: no epilogue stores
     constexpr int GPR = C::BN / 8;
+    GnTileSums<GNM, GPR> gs;
+    if constexpr (GNM != 0) gs.init(p, n0 + (int)(threadIdx.x % GPR) * 8);
     for (int g = threadIdx.x; g < C::BM * GPR; g += 256) {
       const int pl = g / GPR, cg = g - (g / GPR) * GPR;
       const int c = n0 + cg * 8;
@@ -367,26 +372,45 @@ struct SkinnyBlock {
       }
       float v[8];
       load8(es + pl * C::LDE + cg * 8, v);
-      epilogue_store(p, m, c, v, false);
+      if constexpr (GNM != 0) {
+        epilogue_values8(p, m, c, v);
+        gs.add(p, m, KT == 9 ? frame : (int)fast_div((unsigned)m, p.gn.t[0].hw_mul, p.gn.t[0].hw_shr), v);
+        store8(p.y + m * p.ldy + c, v);
+      } else {
+        epilogue_store(p, m, c, v, false);
+      }
+    }
+    if constexpr (GNM != 0) {
+      // a halo tile lies in one frame; a row tile [m0, min(m0 + BM, M)) may run across frames
+      int fa = frame, fb = frame;
+      if constexpr (KT == 1) {
+        const long last = min(m0 + C::BM, M) - 1;
+        fa = (int)fast_div((unsigned)m0, p.gn.t[0].hw_mul, p.gn.t[0].hw_shr);
+        fb = (int)fast_div((unsigned)last, p.gn.t[0].hw_mul, p.gn.t[0].hw_shr);
+      }
+      gs.template finish<C::BN>(p, reinterpret_cast<float*>(smem), n0, fa == fb, fa);
     }
   }
 };
 
-template <int KT, int TH, int TW, int NJ, int U>
+template <int KT, int TH, int TW, int NJ, int U, int GNM>
 __global__ __launch_bounds__(256) void conv_skinny_kernel(const ConvGemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[SkinnyCfg<KT, TH, TW, NJ, U>::LDS];
-  SkinnyBlock<KT, TH, TW, NJ, U> blk{p, smem};
+  static_assert(GNM == 0 || SkinnyCfg<KT, TH, TW, NJ, U>::LDS >= (256 * 16 + 2 * 64 * NJ) * 4, "GroupNorm-sum LDS");
+  SkinnyBlock<KT, TH, TW, NJ, U, GNM> blk{p, smem};
   blk.run();
 }
 
 // Two-kernel split-K (splitk < 0): the last-arriving block of a skinny tile would read every split's partial alone
 // (splits x BMP x BN x 4 bytes through one CU, latency- and per-CU-bandwidth-bound); here one block per (tile, 16-pixel
-// fragment row) sums that row's partials in split order (deterministic), adds the bias and runs the epilogue.
-template <int KT, int TH, int TW, int NJ, int U>
+// fragment row) sums that row's partials in split order (deterministic), adds the bias and runs the epilogue (GNM:
+// with the fused GroupNorm statistics of its 16 rows, GnTileSums).
+template <int KT, int TH, int TW, int NJ, int U, int GNM>
 __global__ __launch_bounds__(256) void skinny_reduce_kernel(const ConvGemmParams p) {
   using C = SkinnyCfg<KT, TH, TW, NJ, U>;
   constexpr int FR = C::MI * NJ, WAVE_F = FR * 256, TILE_F = 4 * WAVE_F;
   __shared__ __attribute__((aligned(16))) bf16 es[16 * C::LDE];
+  __shared__ __attribute__((aligned(16))) float red[GNM ? 256 * 16 + 2 * C::BN : 1];
   const int lb = blockIdx.x, ii = blockIdx.y, tiles = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tiles_n = (p.cout + C::BN - 1) / C::BN, tiles_sp = tiles / tiles_n;
@@ -425,6 +449,13 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const ConvGemmParams
   if (p.diag & 64) return;
   constexpr int GPR = C::BN / 8;
   const long M = conv_rows(p);
+  int frame = 0;
+  if constexpr (KT == 9) {
+    const int tiles_x = (p.wout + TW - 1) / TW, tiles_y = (p.hout + TH - 1) / TH;
+    frame = sp / (tiles_y * tiles_x);
+  }
+  GnTileSums<GNM, GPR> gs;
+  if constexpr (GNM != 0) gs.init(p, n0 + (tid % GPR) * 8);
   for (int g = tid; g < 16 * GPR; g += 256) {
     const int r = g / GPR, cg = g - (g / GPR) * GPR;
     const int pl = ii * 16 + r;
@@ -433,7 +464,6 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const ConvGemmParams
     long m;
     if constexpr (KT == 9) {
       const int tiles_x = (p.wout + TW - 1) / TW, tiles_y = (p.hout + TH - 1) / TH;
-      const int frame = sp / (tiles_y * tiles_x);
       const int trem = sp - frame * (tiles_y * tiles_x);
       const int oy = (trem / tiles_x) * TH + pl / TW, ox = (trem - (trem / tiles_x) * tiles_x) * TW + pl % TW;
       if (oy >= p.hout || ox >= p.wout) continue;
@@ -444,7 +474,24 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const ConvGemmParams
     }
     float v[8];
     load8(es + r * C::LDE + cg * 8, v);
-    epilogue_store(p, m, c, v, false);
+    if constexpr (GNM != 0) {
+      epilogue_values8(p, m, c, v);
+      gs.add(p, m, KT == 9 ? frame : (int)fast_div((unsigned)m, p.gn.t[0].hw_mul, p.gn.t[0].hw_shr), v);
+      store8(p.y + m * p.ldy + c, v);
+    } else {
+      epilogue_store(p, m, c, v, false);
+    }
+  }
+  if constexpr (GNM != 0) {
+    // the 16 rows' frames (a halo tile lies in one frame; token rows may run across frames)
+    int fa = frame, fb = frame;
+    if constexpr (KT == 1) {
+      const long first = (long)sp * TH + ii * 16;
+      const long last = min(min(first + 16, (long)sp * TH + C::BM), M) - 1;
+      fa = (int)fast_div((unsigned)first, p.gn.t[0].hw_mul, p.gn.t[0].hw_shr);
+      fb = (int)fast_div((unsigned)max(last, first), p.gn.t[0].hw_mul, p.gn.t[0].hw_shr);
+    }
+    gs.template finish<C::BN>(p, red, n0, fa == fb, fa);
   }
 }
 
@@ -470,7 +517,7 @@ constexpr SkinnyAlgo kSkinnyAlgos[] = {
 constexpr int kNumSkinny = sizeof(kSkinnyAlgos) / sizeof(kSkinnyAlgos[0]);
 
 bool skinny_eligible(const ConvGemmParams& p, int i) {
-  if (i < 0 || i >= kNumSkinny || p.gn.mode != 0 || p.rows || p.geglu) return false;
+  if (i < 0 || i >= kNumSkinny || p.rows || p.geglu) return false;
   const SkinnyAlgo& a = kSkinnyAlgos[i];
   if (p.cin % 64 != 0 || (p.cin / 64) % a.u != 0) return false;
   if (p.c1 < p.cin && p.c1 % 64 != 0) return false;
@@ -482,7 +529,7 @@ bool skinny_eligible(const ConvGemmParams& p, int i) {
          p.win == p.wout && p.ktot == p.cin;
 }
 
-template <int KT, int TH, int TW, int NJ, int U>
+template <int KT, int TH, int TW, int NJ, int U, int GNM>
 int launch_skinny(ConvGemmParams& p, int splits, hipStream_t stream) {
   using Cf = SkinnyCfg<KT, TH, TW, NJ, U>;
   const long M = (long)p.nb * p.hout * p.wout;
@@ -501,24 +548,25 @@ int launch_skinny(ConvGemmParams& p, int splits, hipStream_t stream) {
   p.kps = gps * U;
   p.splits = splits;
   p.sk_blocks = (sep && splits > 1) ? -1 : 0;
-  hipLaunchKernelGGL((conv_skinny_kernel<KT, TH, TW, NJ, U>), dim3(tiles, splits), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((conv_skinny_kernel<KT, TH, TW, NJ, U, GNM>), dim3(tiles, splits), dim3(256), 0, stream, p);
   DC_CHECK_LAUNCH();
   if (p.sk_blocks < 0) {
-    hipLaunchKernelGGL((skinny_reduce_kernel<KT, TH, TW, NJ, U>), dim3(tiles, Cf::MI), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((skinny_reduce_kernel<KT, TH, TW, NJ, U, GNM>), dim3(tiles, Cf::MI), dim3(256), 0, stream, p);
     DC_CHECK_LAUNCH();
   }
   return DC_OK;
 }
 
-// launch of variant i, for the variants with KT taps (conv_skinny9.hip / conv_skinny1.hip instantiate them)
-template <int KT>
+// launch of variant i, for the variants with KT taps (conv_skinny9.hip / conv_skinny1.hip instantiate them; the
+// fused GroupNorm-statistics forms GNM 1 / 2 in conv_skinny{9,1}_gn.hip)
+template <int KT, int GNM>
 int launch_skinny_idx(int i, ConvGemmParams& p, int splits, hipStream_t s) {
   switch (i) {
 #define DC_SKINNY(i)                                                                                         \
   case i:                                                                                                    \
     if constexpr (kSkinnyAlgos[i].kt == KT)                                                                  \
       return launch_skinny<kSkinnyAlgos[i].kt, kSkinnyAlgos[i].th, kSkinnyAlgos[i].tw, kSkinnyAlgos[i].nj,   \
-                           kSkinnyAlgos[i].u>(p, splits, s);                                                 \
+                           kSkinnyAlgos[i].u, GNM>(p, splits, s);                                            \
     return DC_ERR_ARG;
     DC_SKINNY(0) DC_SKINNY(1) DC_SKINNY(2) DC_SKINNY(3) DC_SKINNY(4) DC_SKINNY(5) DC_SKINNY(6) DC_SKINNY(7)
     DC_SKINNY(8) DC_SKINNY(9) DC_SKINNY(10) DC_SKINNY(11)

@@ -212,15 +212,15 @@ def halo_eligible(d) -> bool:
 
 def skinny_eligible(d) -> bool:
     """Shapes the weight-streaming skinny variants serve (conv_skinny.h skinny_eligible, before the per-variant
-    chunk-group condition): the halo contract, or a 1x1 / linear over whole 64-channel chunks, with no fused
-    GroupNorm statistics; tuned only for the few-pixel layers (at most 512 output pixels: UNet levels 2-3 at batch 1,
-    where dc_gn_fuse_pays keeps the separate GroupNorm -- the first, tuning call of a shape runs before its GroupNorm
-    consumers register, so a fused-statistics conv looks unfused there and the variant would fall back in the step)."""
-    if d.gn or d.nb * d.hout * d.wout > 512:
-        return False
+    chunk-group condition): the halo contract, or a 1x1 / linear over whole 64-channel chunks.  The 1x1 forms are
+    tuned only for the few-pixel layers (at most 512 output pixels: UNet levels 2-3 at batch 1); the 3x3 forms at
+    every size (the weight-in-VGPR ring with one barrier per chunk group beats the per-tap-barrier halo tiles on the
+    level-0 / level-1 convs, profiles/r05af/).  Both carry the fused-GroupNorm-statistics epilogue (conv_skinny.h
+    GnTileSums), so a shape's choice serves its fused and unfused calls alike."""
     if d.kh == 1 and d.kw == 1:
-        return (d.stride == 1 and d.pad == 0 and d.mode == 0 and d.cin % 64 == 0 and d.ktot == d.cin and not d.rows
-                and not d.geglu and d.hin == d.hout and d.win == d.wout and (not d.x2 or d.c1 % 64 == 0))
+        return (d.nb * d.hout * d.wout <= 512 and d.stride == 1 and d.pad == 0 and d.mode == 0 and d.cin % 64 == 0
+                and d.ktot == d.cin and not d.rows and not d.geglu and d.hin == d.hout and d.win == d.wout
+                and (not d.x2 or d.c1 % 64 == 0))
     return halo_eligible(d)
 
 
@@ -256,9 +256,9 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     if halo_eligible(d) and d.cin == 64 and d.cout <= 64 and not d.gn and not d.x2:
         cands += [(a, b) for a in range(RESIDENT_FIRST, WIDE_FIRST) for b in (0, 1, 2, 3)]
     if d.gn:
-        # a GroupNorm-fused call runs skinny / resident / wide choices as the library heuristic (those kernels have
-        # no fused-statistics epilogue): never offer them, so the table only holds configurations that were timed
-        cands = [c for c in cands if not SKINNY_FIRST <= c[0] <= WIDE_LAST]
+        # a GroupNorm-fused call runs resident / wide choices as the library heuristic (those kernels have no
+        # fused-statistics epilogue): never offer them, so the table only holds configurations that were timed
+        cands = [c for c in cands if not RESIDENT_FIRST <= c[0] <= WIDE_LAST]
     if d.ln:
         # a LayerNorm-folded linear (dc_conv_gemm's ln branch) runs on the im2col tiles only: any other choice would be
         # replaced by the library heuristic, so the table would store an id whose timing was the heuristic's

@@ -56,8 +56,11 @@ def group_stats(y, n, hw, c, groups=G):
     return v.mean(-1), v.var(-1, unbiased=False)
 
 
-# conv variants: (algo, nsplit) -- im2col tiles plain / split-K / stream-K, and halo tiles plain / split
-VARIANTS = [(3, 1), (13, 2), (10, 1), (1, -1), (18, 1), (23, 1), (29, 2), (31, 1), (33, 3), (62, 1), (63, 2), (64, 1)]
+# conv variants: (algo, nsplit) -- im2col tiles plain / split-K / stream-K, halo tiles plain / split, and the skinny
+# halo tiles (43 ..: 9 x 12 / 9 x 24 / 6 x 24 pixels, 64 or 128 channels) plain, last-arriver split (> 0) and
+# two-kernel split (< 0, the statistics in skinny_reduce_kernel)
+VARIANTS = [(3, 1), (13, 2), (10, 1), (1, -1), (18, 1), (23, 1), (29, 2), (31, 1), (33, 3), (62, 1), (63, 2), (64, 1),
+            (43, 1), (44, 2), (45, -2), (46, -2), (47, 1)]
 
 
 @pytest.mark.parametrize("algo,nsplit", VARIANTS)
@@ -126,10 +129,13 @@ def test_fused_concat_two_producers(ctx):
     assert rel(nchw(yb, n, h, w), refb) < 1e-2
 
 
-@pytest.mark.parametrize("n,t,c,algo", [(3, 108, 320, 3), (8, 432, 1280, 10), (3, 108, 64, 13), (5, 36, 640, 0)])
-def test_fused_linear_frames_straddle(ctx, n, t, c, algo):
+@pytest.mark.parametrize("n,t,c,algo,nsplit", [(3, 108, 320, 3, 1), (8, 432, 1280, 10, 1), (3, 108, 64, 13, 1),
+                                               (5, 36, 640, 0, 0), (3, 108, 320, 49, 1), (3, 108, 320, 49, -2),
+                                               (8, 432, 1280, 53, 1), (5, 36, 640, 51, 2), (5, 36, 640, 52, -2)])
+def test_fused_linear_frames_straddle(ctx, n, t, c, algo, nsplit):
     """A linear over n * T token rows (T not a multiple of the tile's wave rows): waves whose rows straddle two
-    frames add per row; per-frame statistics exact, results bitwise repeatable."""
+    frames add per row; per-frame statistics exact, results bitwise repeatable.  The skinny row tiles (49 ..: 112 /
+    224 / 64 rows) straddle frames in their own epilogue and in skinny_reduce_kernel's 16-row fragments."""
     from depth_completion_amd import ops
     k = 256
     a = rnd(n * t, k, seed=13).to(torch.bfloat16)
@@ -139,13 +145,17 @@ def test_fused_linear_frames_straddle(ctx, n, t, c, algo):
     for _ in range(2):
         acc = acc_for(n)
         y = torch.empty(n * t, c, dtype=torch.bfloat16, device=dev)
-        ops.linear(ctx, a, wl, n * t, c, y, resid=res, algo=algo or None, nsplit=1 if algo else None,
+        ops.linear(ctx, a, wl, n * t, c, y, resid=res, algo=algo or None, nsplit=nsplit or None,
                    gn=ops.gn_fuse_fwd([(acc, 0, G, c // G, t)]))
         runs.append((y, acc))
     torch.cuda.synchronize()
     y, acc = runs[0]
     # the block finishing a split tile (its last arriver) picks the replica, so compare the replica sums
     assert torch.equal(runs[1][0], y) and torch.equal(runs[1][1].view(4, -1).sum(0), acc.view(4, -1).sum(0))
+    y0 = torch.empty_like(y)   # the fused epilogue stores what the plain one stores
+    ops.linear(ctx, a, wl, n * t, c, y0, resid=res, algo=algo or None, nsplit=nsplit or None)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y)
     gamma = torch.ones(c, device=dev)
     beta = torch.zeros(c, device=dev)
     out = torch.empty_like(y)
@@ -158,7 +168,8 @@ def test_fused_linear_frames_straddle(ctx, n, t, c, algo):
 
 @pytest.mark.parametrize("silu,two,algo,nsplit", [(True, False, 3, 1), (True, True, 13, 2), (False, False, 1, -1),
                                                   (True, False, 31, 1), (True, True, 29, 2), (True, False, 62, 1),
-                                                  (True, True, 63, 2), (False, False, 64, 1)])
+                                                  (True, True, 63, 2), (False, False, 64, 1), (True, False, 43, 1),
+                                                  (True, True, 44, -2), (False, False, 46, 2), (True, True, 47, -2)])
 def test_fused_backward(ctx, silu, two, algo, nsplit):
     """Mode 2: the conv producing dL/d(GN(+SiLU) output) stores dy' and sums (gamma dy', gamma dy' xhat); the
     one-pass backward then matches torch autograd and the separate-pass kernels."""
