@@ -275,6 +275,7 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
     if cold and getattr(ctx, "_flush", None) is None:
         ctx._flush = torch.empty(512 << 20, dtype=torch.uint8, device=ctx.device)
         ctx._sink = torch.empty((), dtype=torch.float32, device=ctx.device)
+    timed = []
     for a, s in cands:
         dt.algo, dt.splitk = a, s
         try:
@@ -303,6 +304,9 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
             t = e0.elapsed_time(e1)
         if t < best_t * 0.97:  # prefer the earlier (heuristic / fewer splits) on near-ties
             best, best_t = (a, s), t
+        timed.append((t / reps * 1e3, a, s))
+    if getattr(ctx, "tune_top", None) is not None:   # tools/tune_gemm.py --top-out: the runners-up, fastest first
+        ctx.tune_top[conv_key(d)] = [(a, s, round(us, 2)) for us, a, s in sorted(timed)[:6]]
     print(f"tuned {conv_key(d)} -> {best} ({best_t / reps * 1e3:.1f} us)", file=sys.stderr,
           flush=True)
     return best

@@ -52,7 +52,8 @@ def record(out, batch):
             d = ConvDesc.from_buffer_copy(a[0]._obj)
             descs.append(dict(M=d.nb * d.hout * d.wout, rows=int(d.nrows) if d.rows else 0, N=d.cout,
                               K=d.kh * d.kw * d.cin, cin=d.cin, mode=d.mode, k=d.kh, stride=d.stride,
-                              hw=[d.hout, d.wout], algo=int(d.algo), split=int(d.splitk), flops=conv_flops(d)))
+                              hw=[d.hout, d.wout], algo=int(d.algo), split=int(d.splitk), flops=conv_flops(d),
+                              key=[int(v) for v in ops.conv_key(d)]))
         return orig(name, *a)
 
     # the captured step's launch sequence: record while capturing a throwaway graph (nothing runs)
@@ -70,7 +71,7 @@ def record(out, batch):
     print(f"{len(descs)} conv launches per step recorded", flush=True)
 
 
-def analyse(trace, descs_path):
+def analyse(trace, descs_path, keys_out=None):
     descs = json.load(open(descs_path))
     rows = []
     with open(trace) as f:
@@ -93,8 +94,8 @@ def analyse(trace, descs_path):
     best = None
     for off in range(0, min(len(conv) - n, 200) + 1):
         win = conv[len(conv) - n - off:len(conv) - off]
-        fam = lambda a: ("halo" if 23 <= a <= 36 else "skinny" if 43 <= a <= 54 else "resident" if a >= 55  # noqa: E731
-                         else "gemm")
+        fam = lambda a: ("halo" if 23 <= a <= 36 or 62 <= a <= 66 else "skinny" if 43 <= a <= 54  # noqa: E731
+                         else "resident" if 55 <= a <= 58 else "gemm")
         ok = sum(fam(d["algo"]) in w[2] for w, d in zip(win, descs))
         if best is None or ok > best[0]:
             best = (ok, win)
@@ -114,6 +115,16 @@ def analyse(trace, descs_path):
         g[3].add((d["algo"], d["split"]))
         tot += us
     print(f"conv time in one step: {tot / 1e3:.3f} ms over {n} launches")
+    if keys_out:   # per table key: launches, us in the step, the (algo, split) it ran
+        per = defaultdict(lambda: [0, 0.0, None])
+        for (s, e, name), d in zip(win, descs):
+            if "key" in d:
+                k = json.dumps(d["key"])
+                per[k][0] += 1
+                per[k][1] += (e - s) / 1e3
+                per[k][2] = [d["algo"], d["split"]]
+        with open(keys_out, "w") as f:
+            json.dump(per, f, indent=0)
     for key, (cnt, us, fl, algos) in sorted(groups.items(), key=lambda kv: -kv[1][1]):
         M, N, K, mode, k, stride, rl = key
         print(f"M={M:7d}{'r' if rl else ' '} N={N:5d} K={K:6d} mode={mode} k={k} s={stride} x{cnt:3d}: {us:8.1f} us "
@@ -126,9 +137,10 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--trace")
     ap.add_argument("--descs")
+    ap.add_argument("--keys-out", help="(with --trace) per-table-key step time as JSON")
     a = ap.parse_args()
     if a.trace:
-        analyse(a.trace, a.descs)
+        analyse(a.trace, a.descs, a.keys_out)
     else:
         record(a.out, a.batch)
 

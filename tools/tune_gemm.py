@@ -11,6 +11,7 @@ Usage: python tools/tune_gemm.py [--workloads c2:1 c2:8 c4:1 c4:8 c5:1] [--out d
   points, run as the 10-seed ensemble (one batch-10 call per frame, the shapes C5 launches)
 """
 import argparse
+import json
 import os
 import sys
 
@@ -34,6 +35,8 @@ def main():
     ap.add_argument("--try", dest="try_algos", type=int, nargs="+",
                     help="re-time every shape of the workloads: its committed choice against these algo ids (all "
                          "their splits) only; shapes outside the workloads keep their entries")
+    ap.add_argument("--top-out", help="also write every re-timed shape's six fastest variants (isolated timing) here, "
+                    "the candidates tools/ab/instep_tables.py evaluates inside the step")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     pipe = MarigoldDepthCompletionPipeline(synthetic.unet_state_dict(MARIGOLD_V1, 11), synthetic.taesd_state_dict(12),
@@ -51,6 +54,8 @@ def main():
         pipe.ctx.tune_only = (set(args.try_algos), committed)
         pipe.ctx.algo_cache = {}
     pipe.ctx.tune = True
+    if args.top_out:
+        pipe.ctx.tune_top = {}
     shapes = {"c2": (576, 768, 500, "uniform"), "c3": (576, 768, 500, "uniform"), "c4": (352, 1216, 0, "beams"),
               "c5": (900, 1600, 3000, "uniform")}
     for wl in args.workloads:
@@ -72,6 +77,9 @@ def main():
         print(f"--try {args.try_algos}: {changed} of {len(pipe.ctx.algo_cache)} re-timed shapes changed", flush=True)
         pipe.ctx.algo_cache = {**committed, **pipe.ctx.algo_cache}
     ops.save_tuned(pipe.ctx.algo_cache, args.out)
+    if args.top_out:
+        with open(args.top_out, "w") as f:
+            json.dump([{"key": list(k), "top": [list(c) for c in v]} for k, v in sorted(pipe.ctx.tune_top.items())], f)
     for k, v in sorted(pipe.ctx.algo_cache.items()):
         print(k, v)
 
