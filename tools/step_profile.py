@@ -17,7 +17,7 @@ from collections import defaultdict
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def record(out, batch):
+def record(out, batch, frame=(576, 768, 500, "uniform")):
     import threading
     import time
     import torch
@@ -37,13 +37,15 @@ def record(out, batch):
     dev = torch.device("cuda:0")
     pipe = MarigoldDepthCompletionPipeline(synthetic.unet_state_dict(MARIGOLD_V1, 11), synthetic.taesd_state_dict(12),
                                            synthetic.text_embedding(13, 1024), device=dev)
-    fr = [synth_frame(576, 768, 500, i) for i in range(batch)]
+    h, w, npts, pattern = frame
+    # C5 is a batch-10 call of one frame (the seed ensemble's shapes); other batches take distinct frames
+    fr = [synth_frame(h, w, npts, 0 if batch == 10 else i, pattern) for i in range(batch)]
     imgs = torch.stack([f[0] for f in fr]).to(dev)
     sps = torch.stack([f[1] for f in fr]).to(dev)
     for _ in range(2):
         pipe(imgs, sps, 120.0, norm="const", steps=8, resolution=768)
     torch.cuda.synchronize()
-    st = pipe._plans[(batch, 72, 96)]
+    st = next(v for k, v in pipe._plans.items() if k[0] == batch)
     descs = []
     orig = ops.call
 
@@ -135,6 +137,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out")
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--frame", default="576,768,500,uniform",
+                    help="height,width,points,pattern of the synthetic frame (C4: 352,1216,0,beams; C5 with "
+                         "--batch 10: 900,1600,3000,uniform)")
     ap.add_argument("--trace")
     ap.add_argument("--descs")
     ap.add_argument("--keys-out", help="(with --trace) per-table-key step time as JSON")
@@ -142,7 +147,8 @@ def main():
     if a.trace:
         analyse(a.trace, a.descs, a.keys_out)
     else:
-        record(a.out, a.batch)
+        h, w, n, pat = a.frame.split(",")
+        record(a.out, a.batch, (int(h), int(w), int(n), pat))
 
 
 if __name__ == "__main__":
