@@ -2,9 +2,9 @@
 epilogue, and that misranks some shapes for the graph-replayed step (profiles/r05ag/).  Here the runners-up are
 timed inside the step instead.
 
-  make <committed.json> <top.json> <out_prefix> [n]
-      Write n alternative tables (default 3).  Table i gives every shape its i-th fastest isolated variant that
-      differs from the committed choice; a shape with fewer runners-up keeps the committed choice.  A table changes
+  make <committed.json> <top.json> <out_prefix> [n] [skip]
+      Write n alternative tables (default 3).  Table i gives every shape its (skip + i)-th fastest isolated variant
+      that differs from the committed choice; a shape with fewer runners-up keeps the committed choice.  A table changes
       every shape at once, so one step profile per table times one alternative for every shape.
   pick <committed.json> <out.json> <keys_committed.json> <table_1.json> <keys_1.json> [<table_2.json> <keys_2.json> ...]
       keys_*.json come from tools/step_profile.py --keys-out over each table.  Each shape takes the table whose
@@ -24,7 +24,7 @@ def save(table, path):
               indent=0)
 
 
-def make(committed, top, prefix, n=3):
+def make(committed, top, prefix, n=3, skip=0):
     base = load(committed)
     tops = {tuple(e["key"]): [(c[0], c[1]) for c in e["top"]] for e in json.load(open(top))}
     for i in range(1, n + 1):
@@ -32,11 +32,11 @@ def make(committed, top, prefix, n=3):
         changed = 0
         for k, cands in tops.items():
             alts = [c for c in cands if c != base.get(k)]
-            if k in base and len(alts) >= i:
-                t[k] = alts[i - 1]
+            if k in base and len(alts) >= skip + i:
+                t[k] = alts[skip + i - 1]
                 changed += 1
         save(t, f"{prefix}{i}.json")
-        print(f"{prefix}{i}.json: {changed} shapes on their runner-up {i}")
+        print(f"{prefix}{i}.json: {changed} shapes on their runner-up {skip + i}")
 
 
 def pick(committed, out, keys0, rest):
@@ -62,6 +62,7 @@ def pick(committed, out, keys0, rest):
 
 if __name__ == "__main__":
     if sys.argv[1] == "make":
-        make(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]) if len(sys.argv) > 5 else 3)
+        make(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]) if len(sys.argv) > 5 else 3,
+             int(sys.argv[6]) if len(sys.argv) > 6 else 0)
     else:
         pick(sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5:])
