@@ -1,7 +1,7 @@
 """Probe (GPU, timing only): the level-2 / level-3 skinny convs with and without the fused GroupNorm statistics
 (dc_gn_fuse modes 1 / 2) in their epilogues, and the diagnostic arms that skip parts of it (DC_HALO_DIAG 8: no
 accumulator adds; 16: no block fold either), each call timed inside a 20-call graph.
-Args: [skinny | halo] (the level-2 / 3 skinny shapes, or level-0 / 1 halo shapes)."""
+Args: [skinny | halo | l01] (the level-2 / 3 skinny shapes, level-0 / 1 halo shapes, or level-0 / 1 halo vs skinny)."""
 import math
 import os
 import sys
@@ -45,7 +45,10 @@ def r(*s):
 
 SHAPES = {"skinny": [(9, 12, 1280, 43, -10), (9, 12, 1280, 43, 10), (9, 12, 1280, 43, 1), (18, 24, 1280, 47, -4),
                      (18, 24, 640, 47, -4)],
-          "halo": [(72, 96, 320, 33, 1), (36, 48, 640, 31, 3), (36, 48, 640, 33, 1), (72, 96, 640, 62, 1)]}
+          "halo": [(72, 96, 320, 33, 1), (36, 48, 640, 31, 3), (36, 48, 640, 33, 1), (72, 96, 640, 62, 1)],
+          # level-0 / 1: the skinny form against the halo tile it replaced or kept (profiles/r05ag/)
+          "l01": [(72, 96, 320, 33, 1), (72, 96, 320, 47, 1), (72, 96, 640, 62, 1), (72, 96, 640, 47, 1),
+                  (36, 48, 1280, 31, 5), (36, 48, 1280, 47, 1)]}
 for h, w, c, algo, ns in SHAPES[sys.argv[1] if len(sys.argv) > 1 else "skinny"]:
     x = r(h * w, c)
     wt = pack_conv(torch.randn(c, c, 3, 3) / math.sqrt(9 * c)).to(dev, torch.bfloat16)
