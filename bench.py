@@ -495,7 +495,10 @@ def run_worker(args) -> None:
                 roofline["traffic_per_step"] = round(pmc["traffic_bytes_per_step"])
                 # counter bytes over the launches' own operands moved once: the re-fetch factor beyond L2
                 roofline["traffic_over_algorithmic"] = round(pmc["traffic_bytes_per_step"] / conv_bytes_, 2)
-            if pmc.get("mfma_busy_cycles_per_step") is not None:
+            from depth_completion_amd.build import conv_family_hash
+            current = pmc.get("conv_family_hash") == conv_family_hash()
+            roofline["pmc_current"] = current   # counters taken on this tree's conv kernels and tuned table
+            if pmc.get("mfma_busy_cycles_per_step") is not None and current:
                 # MFMA-busy cycles of the step's conv family over that family's graph-replayed time at the peak
                 # clock x 1024 SIMDs: one v_mfma_f32_16x16x32_bf16 (16 K FLOP) keeps a SIMD busy 16 cycles, so this
                 # is >= frac by construction (it counts padding and split-hi/lo MFMAs that frac does not)

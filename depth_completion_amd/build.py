@@ -44,6 +44,22 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+CONV_FAMILY = ["conv_gemm.hip", "conv_gemm_gn.hip", "conv_gemm_gnb.hip", "conv_gemm_ln.hip", "conv_skinny9.hip",
+               "conv_skinny1.hip", "conv_skinny9_gn.hip", "conv_skinny9_gnb.hip", "conv_skinny1_gn.hip",
+               "conv_skinny1_gnb.hip", "conv_gemm_impl.h", "conv_skinny.h", "gn_acc.h", "common.h"]
+
+
+def conv_family_hash() -> str:
+    """sha256 prefix over the conv family's kernel sources and the tuned variant table: the provenance a committed PMC
+    record of that family carries (tools/pmc_step.py), so that bench.py pairs its counters only with the same kernels
+    and variant choices (any other change to the library leaves the conv counters valid)."""
+    h = hashlib.sha256()
+    for name in CONV_FAMILY:
+        h.update(name.encode() + b"\0" + (CSRC / name).read_bytes() + b"\0")
+    h.update((PKG / "tuned_gfx950.json").read_bytes())
+    return h.hexdigest()[:16]
+
+
 def _includes(src: Path, seen: set | None = None) -> set:
     """The repo headers a source includes, transitively (#include "..."): a header edit rebuilds only its users."""
     seen = set() if seen is None else seen

@@ -166,7 +166,9 @@ extern "C" int dc_conv_gemm(const dc_conv_desc* d, void* stream) {
     // wide im2col tile: the launch below (algo_index maps it into kAlgos).  No fused-GroupNorm form: a GroupNorm-fused
     // call that carries a wide choice (the table's entry is shared with the shape's unfused calls, and a shape is
     // tuned before its GroupNorm consumers register) runs the 64 x 64 double-buffered tile, the level-0 winner before
-    if (p.gn.mode != 0) {
+    // A folded FF2 / proj_out input-gradient (geglu_n) splits its epilogue per column tile at geglu_n, a multiple of
+    // 256: a 320-wide tile can straddle it (4C = 256 / 512 for C = 64 / 128), so it takes that tile too.
+    if (p.gn.mode != 0 || p.geglu_n != 0) {
       algo = 13;
       splits = 1;
     }

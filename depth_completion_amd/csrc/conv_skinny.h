@@ -487,6 +487,9 @@ __global__ __launch_bounds__(256) void skinny_reduce_kernel(const ConvGemmParams
     int fa = frame, fb = frame;
     if constexpr (KT == 1) {
       const long first = (long)sp * TH + ii * 16;
+      // a trailing 16-row fragment of the last tile can start past the last row (M = 108 on 128-row tiles): it stored
+      // nothing, so it adds nothing -- return (block-uniform) rather than form a frame index past the last frame
+      if (first >= M) return;
       const long last = min(min(first + 16, (long)sp * TH + C::BM), M) - 1;
       fa = (int)fast_div((unsigned)first, p.gn.t[0].hw_mul, p.gn.t[0].hw_shr);
       fb = (int)fast_div((unsigned)max(last, first), p.gn.t[0].hw_mul, p.gn.t[0].hw_shr);

@@ -10,9 +10,11 @@
 //   dc_fold_linear_pair      FF2 and proj_out of a transformer block folded into one two-source linear
 //   dc_conv_pick             the tuned GEMM variant of a conv shape, nearest tuned shape for shapes not in the table
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -138,10 +140,22 @@ extern "C" int dc_fold_linear_pair(const float* w2, const float* b2, int c, int 
     memcpy(&u, &f, 4);
     return (uint16_t)(u >> 16);
   };
-  std::vector<double> w2d((size_t)c * k2);
+  std::vector<double> w2d;
+  try {
+    w2d.resize((size_t)c * k2);
+  } catch (...) {
+    return 1;
+  }
   for (size_t e = 0; e < w2d.size(); ++e) w2d[e] = (double)round_bf16(w2[e]);
+  std::atomic<int> failed{0};
   auto rows = [&](int r0, int r1) {
-    std::vector<double> acc((size_t)k2);
+    std::vector<double> acc;
+    try {
+      acc.resize((size_t)k2);
+    } catch (...) {   // a thread body must not throw (std::terminate)
+      failed = 1;
+      return;
+    }
     for (int i = r0; i < r1; ++i) {   // row i of Wp W2: sum_m Wp[i][m] W2[m][.], m ascending
       std::fill(acc.begin(), acc.end(), 0.0);
       for (int m = 0; m < c; ++m) {
@@ -164,14 +178,28 @@ extern "C" int dc_fold_linear_pair(const float* w2, const float* b2, int c, int 
       bias[i] = (float)bb;
     }
   };
-  const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
-  std::vector<std::thread> th;
-  for (int t = 0; t < nt; ++t) {
-    const int r0 = (int)((long)c * t / nt), r1 = (int)((long)c * (t + 1) / nt);
-    if (r1 > r0) th.emplace_back(rows, r0, r1);
+  // nothing may cross the C ABI: a failed thread creation runs the remaining rows on this thread (each row is summed
+  // in a fixed order, so the bits do not depend on the split), and an allocation failure returns nonzero
+  try {
+    const int nt = std::max(1, std::min(16, (int)std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    int done = 0;   // rows [0, done) handed to threads
+    for (int t = 0; t < nt; ++t) {
+      const int r0 = (int)((long)c * t / nt), r1 = (int)((long)c * (t + 1) / nt);
+      if (r1 <= r0) continue;
+      try {
+        th.emplace_back(rows, r0, r1);
+        done = r1;
+      } catch (const std::system_error&) {
+        break;
+      }
+    }
+    for (auto& x : th) x.join();
+    if (done < c) rows(done, c);
+  } catch (...) {
+    return 1;
   }
-  for (auto& x : th) x.join();
-  return 0;
+  return failed ? 1 : 0;
 }
 
 extern "C" int dc_fold_cross_attention(const float* wq, const float* wk, const float* wv, const float* wo,

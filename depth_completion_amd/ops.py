@@ -259,6 +259,10 @@ def _autotune(ctx: Ctx, d, y, reps: int = 3, srcs=()) -> tuple:
         # a GroupNorm-fused call runs resident / wide choices as the library heuristic (those kernels have no
         # fused-statistics epilogue): never offer them, so the table only holds configurations that were timed
         cands = [c for c in cands if not RESIDENT_FIRST <= c[0] <= WIDE_LAST]
+    if d.geglu_n:
+        # the folded FF2 / proj_out input-gradient runs wide (320-column) choices as the 64 x 64 tile (a wide tile can
+        # straddle geglu_n, where the epilogue switches from the GEGLU backward to plain stores): never offer them
+        cands = [c for c in cands if not WIDE_FIRST <= c[0] <= WIDE_LAST]
     if d.ln:
         # a LayerNorm-folded linear (dc_conv_gemm's ln branch) runs on the im2col tiles only: any other choice would be
         # replaced by the library heuristic, so the table would store an id whose timing was the heuristic's
@@ -411,6 +415,8 @@ def attn_fwd(ctx: Ctx, qkv, nb, t, heads, o, lse):
 
 
 def attn_bwd(ctx: Ctx, qkv, o, dout, lse, nb, t, heads, delta, dqkv):
+    if delta.numel() < 2 * nb * heads * t:   # ABI 21: -delta and -8 lse, the dK/dV kernel's row constants
+        raise ValueError(f"attn_bwd: delta workspace holds {delta.numel()} floats, needs 2 * nb * heads * t")
     call("dc_attn_bwd", P(qkv), LD(qkv), P(o), LD(o), P(dout), LD(dout), lse.data_ptr(), nb, t, heads,
          delta.data_ptr(), P(dqkv), LD(dqkv), ctx.ws.data_ptr(), ctx.ws_bytes, ctx.stream)
     return dqkv

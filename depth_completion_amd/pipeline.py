@@ -404,7 +404,7 @@ class MarigoldDepthCompletionPipeline:
         if self.use_graph:
             g = st["graph"]
             gkey = (guided, guided and cf, opt_code, kld_code, float(kld_weight), steps, H, W, RH, RW, lr_latent,
-                    lr_scaling, loss_flags if full_loss else 0, row_counts)
+                    lr_scaling, loss_flags if full_loss else 0, row_counts, self._scheduler_key())
             if g is None or st["graph_key"] != gkey:
                 # (re)capture: the graph binds this call's tables -- the plan's persistent guide buffers for (n, H, W)
                 # and the kept (steps, lr, optimiser) tables, which later calls with the same key rewrite in place
@@ -594,12 +594,17 @@ class MarigoldDepthCompletionPipeline:
     def _step_tables(self, steps, lr_latent, lr_scaling, opt_code):
         """(timesteps (host), DDIM coefficients, optimiser scalars (device)) for a step count, learning rates and
         optimiser; kept, so that repeated calls neither recompute them nor copy them to the device."""
-        key = (int(steps), float(lr_latent), float(lr_scaling), int(opt_code), repr(sorted(self.scheduler.config.items())))
+        key = (int(steps), float(lr_latent), float(lr_scaling), int(opt_code), self._scheduler_key())
         cache = self.__dict__.setdefault("_step_table_cache", {})
         if key not in cache:
+            if len(cache) >= 64:   # bounded like _noise; a captured graph keeps its own tables alive (graph_tables)
+                cache.clear()
             ts, coef, adam = self.scheduler._tables(steps, (lr_latent, lr_scaling), opt_code)
             cache[key] = (ts, coef.to(self.device), adam.to(self.device))
         return cache[key]
+
+    def _scheduler_key(self):
+        return repr(sorted(self.scheduler.config.items()))
 
     def _vae_input(self, lat_ptr, P, dp):
         """decode_prediction's VAE input from the latents at lat_ptr ([P][8] rows, 4 channels): TAESD's

@@ -15,9 +15,13 @@ Usage: python tools/pmc_step.py <fetch.csv> <write.csv> <mfma.csv> <descs.json> 
 """
 import csv
 import json
+import os
 import re
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from depth_completion_amd.build import conv_family_hash  # noqa: E402
 
 FAMILY = re.compile(r"conv_(gemm|halo|skinny|resident)_kernel|skinny_reduce")
 LAUNCH = re.compile(r"conv_(gemm|halo|skinny|resident)_kernel")
@@ -55,6 +59,8 @@ def main():
     write_b = 1024.0 * w["WRITE_SIZE"]
     res = {
         "population": "conv family of the last complete graph-replayed guided step (tools/step_profile.py)",
+        # kernel sources + tuned table the counters were taken on; bench.py reports mfma_util only on a match
+        "conv_family_hash": conv_family_hash(),
         "kernel_regex": FAMILY.pattern,
         "dc_conv_gemm_calls_per_step": n_calls,
         "family_dispatches_per_step": [nf, nw, nm],
