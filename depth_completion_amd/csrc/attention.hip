@@ -231,6 +231,16 @@ __device__ __forceinline__ void vm_wait_n() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// The ring's per-tile barrier.  The caller's counted vm_wait_n has landed this wave's pieces of the tile; the barrier
+// makes every wave's pieces visible, and the lgkmcnt(0) ahead of it retires this wave's reads of the stage the next
+// DMA overwrites.  No workgroup fence: __syncthreads() is a release fence as well, lowered with a vmcnt(0) that also
+// waits for the LDS-DMA of the LATER tiles, i.e. drains the ring's prefetch at every tile.
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 struct AttnSK {
   float* slab;     // [G * spb slots][QW waves][NV values][64 lanes] fp32 partials
   int* counters;   // one per key- / query-block (global index), zero between launches
@@ -394,7 +404,7 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
     constexpr int ST = decltype(STC)::value;
     if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();  // S = 3: at most one younger tile in flight
     else vm_wait_n<0>();
-    __syncthreads();
+    ring_barrier();
     if (i + S - 1 < mine) issue(i + S - 1);
     if (i < mine) {
       const int kt = tb + i;
@@ -551,7 +561,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 // ------------------------------------------------------------------------------ backward
 // dK/dV: 32 QW keys per block resident in registers (32 per wave); KS query-splits per block (waves
 // QW p .. QW p + QW - 1 sweep the p-th range of query tiles), partial dK/dV folded through LDS in a
-// fixed order.  Q / dO tiles (+ lse / delta rows) stream through an LDS-DMA ring; Q is not pre-scaled
+// fixed order.  Q / dO tiles (+ the rows' -8 lse / -delta) stream through an LDS-DMA ring; Q is not pre-scaled
 // (the 1/8 softmax scale is folded into the exp argument and into dK at the end).
 //
 // Stream-K form (SK, batch-1 shapes whose key-blocks would leave most CUs with one 4-wave block, i.e. one
@@ -565,7 +575,7 @@ __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2)
 constexpr int BWD_S = 3;
 template <int QW, int KS>
 struct DkdvLds {
-  static constexpr int STAGE = 2 * TILE_B + 2 * 64 * 4;     // Q, dO, lse, delta
+  static constexpr int STAGE = 2 * TILE_B + 2 * 64 * 4;     // Q, dO, -8 lse, -delta
   static constexpr int RING = KS * BWD_S * STAGE;
   static constexpr int RED = (KS - 1) * QW * 64 * 64 * 4;
   static constexpr int BYTES = RING > RED ? RING : RED;
@@ -574,7 +584,7 @@ struct DkdvLds {
 // one key-block (kb, h, n) over query tiles [t0, t0 + tcount); SK: segment `seg` of this block's range
 template <int QW, int KS, bool SK>
 __device__ __forceinline__ void dkdv_segment(char* smem, const bf16* qkv, int ld, const bf16* dout, int lddo,
-                                             const float* lse, const float* delta, int T, int heads, bf16* dqkv,
+                                             const float* nl8, const float* ndel, int T, int heads, bf16* dqkv,
                                              int ldd, int kb, int h, int n, int t0, int tcount, const AttnSK& sk,
                                              long bi, int seg) {
   constexpr int NT = 64 * QW;
@@ -587,8 +597,8 @@ __device__ __forceinline__ void dkdv_segment(char* smem, const bf16* qkv, int ld
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
   const bf16* dob = dout + (long)n * T * lddo;
-  const float* lse_b = lse + ((long)n * heads + h) * T;
-  const float* del_b = delta + ((long)n * heads + h) * T;
+  const float* lse_b = nl8 + ((long)n * heads + h) * T;    // -8 lse (raw-score units)
+  const float* del_b = ndel + ((long)n * heads + h) * T;   // -delta
   const int my_k = kb * (32 * QW) + wid * 32 + (lane & 31);
   const bool kok = my_k < T;
   bf16x8 kf[4], vf[4];
@@ -646,27 +656,46 @@ __device__ __forceinline__ void dkdv_segment(char* smem, const bf16* qkv, int ld
   for (int i = 0; i < S - 1 && i < mine; ++i) issue(i);
   auto step = [&](int i, auto STC) __attribute__((always_inline)) {
     constexpr int ST = decltype(STC)::value;
-    if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();  // (wave 0 also has the lse/delta pieces: conservative)
+    if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();  // (wave 0 also has the row-constant pieces: conservative)
     else vm_wait_n<0>();
-    __syncthreads();
+    ring_barrier();
     if (i + S - 1 < mine) issue(i + S - 1);
     if (i < mine) {
       const char* qt_s = ring + ST * STG;
       const char* dt_s = qt_s + TILE_B;
-      const float* ls = reinterpret_cast<const float*>(qt_s + 2 * TILE_B);
-      const float* dl = ls + 64;
+      const float* ls = reinterpret_cast<const float*>(qt_s + 2 * TILE_B);   // -8 lse of the tile's 64 query rows
+      const float* dl = ls + 64;                                           // -delta
+      // Row constants as the initial accumulators (accumulator element r holds query row
+      // 32 qb + 8 (r >> 2) + 4 hh + (r & 3): 4 rows per ds_read_b128): S' = Q K^T - 8 lse and dP' = dO V^T - delta
+      // leave the MFMA chains ready for P = exp2(S' log2e / 8) and dS = P dP' -- no per-score subtraction and no
+      // per-score lse scaling on the VALU.  Both query halves' S / dP are issued first, so the second half's
+      // MFMAs run under the first half's softmax.
+      f32x16 spa[2], dpa[2];
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        // S and dP from zero accumulators; accumulator element r holds query row
-        // 32 qb + 8 (r >> 2) + 4 hh + (r & 3): lse / delta are read 4 rows per ds_read_b128
-        f32x16 sp = {}, dp = {};
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + 32 * qb + 8 * g + 4 * hh);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + 32 * qb + 8 * g + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            spa[qb][4 * g + e] = l4[e];
+            dpa[qb][4 * g + e] = d4[e];
+          }
+        }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(qt_s + qoff[qb][s]), kf[s],
-                                                       sp, 0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(dt_s + qoff[qb][s]), vf[s],
-                                                       dp, 0, 0, 0);
+          spa[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(qt_s + qoff[qb][s]),
+                                                            kf[s], spa[qb], 0, 0, 0);
+          dpa[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(dt_s + qoff[qb][s]),
+                                                            vf[s], dpa[qb], 0, 0, 0);
         }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x16& sp = spa[qb];
+        f32x16& dp = dpa[qb];
         // dO^T / Q^T fragments of the first k-slice, in flight under the softmax
         constexpr int QIMM = ST * STG, DIMM = ST * STG + TILE_B;
         bf16x8 fv[2][2], fk[2][2];
@@ -675,17 +704,12 @@ __device__ __forceinline__ void dkdv_segment(char* smem, const bf16* qkv, int ld
           fv[0][db] = trans_frag_nw<DIMM>(ta[qb][0][db][0], ta[qb][0][db][1]);
           fk[0][db] = trans_frag_nw<QIMM>(ta[qb][0][db][0], ta[qb][0][db][1]);
         }
-        // P = exp2(S_raw log2e / 8 - lse log2e); dS = P * (dP - delta)
+        // P = exp2(S' log2e / 8); dS = P dP'
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(ls + 32 * qb + 8 * g + 4 * hh);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl + 32 * qb + 8 * g + 4 * hh);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float pv = fast_exp2(fmaf(sp[4 * g + e], L8, -l4[e] * LOG2E));
-            sp[4 * g + e] = pv;
-            dp[4 * g + e] = pv * (dp[4 * g + e] - d4[e]);
-          }
+        for (int r = 0; r < 16; ++r) {
+          const float pv = fast_exp2(sp[r] * L8);
+          sp[r] = pv;
+          dp[r] *= pv;
         }
 #pragma unroll
         for (int db = 0; db < 2; ++db) {
@@ -783,19 +807,19 @@ __device__ __forceinline__ void dkdv_segment(char* smem, const bf16* qkv, int ld
 
 template <int QW, int KS, bool SK>
 __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dkdv_kernel(
-    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* lse, const float* delta, int T, int heads,
+    const bf16* qkv, int ld, const bf16* dout, int lddo, const float* nl8, const float* ndel, int T, int heads,
     bf16* dqkv, int ldd, AttnSK sk) {
   __shared__ __attribute__((aligned(16))) char smem[DkdvLds<QW, KS>::BYTES];
   const int ntq = (T + 63) / 64;
   if constexpr (!SK) {
-    dkdv_segment<QW, KS, false>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, blockIdx.x, blockIdx.y,
+    dkdv_segment<QW, KS, false>(smem, qkv, ld, dout, lddo, nl8, ndel, T, heads, dqkv, ldd, blockIdx.x, blockIdx.y,
                                 blockIdx.z, 0, ntq, sk, 0, 0);
   } else {
     const int nkb = (T + 32 * QW - 1) / (32 * QW);
     sk_walk(sk, ntq, [&](long bi, int t0, int cnt, int seg) {
       const int kb = (int)(bi % nkb);
       const long nh = bi / nkb;
-      dkdv_segment<QW, KS, true>(smem, qkv, ld, dout, lddo, lse, delta, T, heads, dqkv, ldd, kb, (int)(nh % heads),
+      dkdv_segment<QW, KS, true>(smem, qkv, ld, dout, lddo, nl8, ndel, T, heads, dqkv, ldd, kb, (int)(nh % heads),
                                  (int)(nh / heads), t0, cnt, sk, bi, seg);
     });
   }
@@ -814,8 +838,9 @@ struct DqLds {
 
 template <int QW, int KS, bool SK>
 __device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, const bf16* o, int ldo,
-                                           const bf16* dout, int lddo, const float* lse, float* delta, int T,
-                                           int heads, bf16* dqkv, int ldd, int qbk, int h, int n, int t0, int tcount,
+                                           const bf16* dout, int lddo, const float* lse, float* ndel, float* nl8,
+                                           int T, int heads, bf16* dqkv, int ldd, int qbk, int h, int n, int t0,
+                                           int tcount,
                                            const AttnSK& sk, long bi, int seg) {
   constexpr int NT = 64 * QW;
   constexpr int S = BWD_S;
@@ -834,10 +859,11 @@ __device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, 
     qf[s] = load_row8(base + (long)my_q * ld + h * 64 + 16 * s + 8 * hh, qok, 0.125f);
     df[s] = load_row8(dout + ((long)n * T + my_q) * lddo + h * 64 + 16 * s + 8 * hh, qok, 1.0f);
   }
-  const float my_lse = qok ? lse[((long)n * heads + h) * T + my_q] * LOG2E : INFINITY;
+  const float lse_nat = qok ? lse[((long)n * heads + h) * T + my_q] : INFINITY;
+  const float my_lse = lse_nat * LOG2E;
   // delta = sum_d dO * O of this lane's query, from the dO fragments already in registers and the same
-  // pieces of O (fp32, fixed order); the key-range segment that starts the row (t0 = 0, part 0) publishes it
-  // for the dK/dV kernel, which runs after this one
+  // pieces of O (fp32, fixed order); the key-range segment that starts the row (t0 = 0, part 0) publishes the
+  // dK/dV kernel's row constants -delta and -8 lse (it runs after this one)
   float my_del = 0.0f;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -846,7 +872,11 @@ __device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, 
     for (int j = 0; j < 8; ++j) my_del = fmaf((float)df[s][j], (float)of[j], my_del);
   }
   my_del += __shfl_xor(my_del, 32, 64);
-  if (qok && hh == 0 && part == 0 && t0 == 0) delta[((long)n * heads + h) * T + my_q] = my_del;
+  if (qok && hh == 0 && part == 0 && t0 == 0) {
+    const long r = ((long)n * heads + h) * T + my_q;
+    ndel[r] = -my_del;
+    nl8[r] = -8.0f * lse_nat;
+  }
   f32x16 dq[2];
 #pragma unroll
   for (int db = 0; db < 2; ++db)
@@ -885,22 +915,30 @@ __device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, 
     constexpr int ST = decltype(STC)::value;
     if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();
     else vm_wait_n<0>();
-    __syncthreads();
+    ring_barrier();
     if (i + S - 1 < mine) issue(i + S - 1);
     if (i < mine) {
       const int kt = tb + i;
       const char* kt_s = ring + ST * STG;
       const char* vt_s = kt_s + TILE_B;
+      // S and dP of both key halves first: the second half's MFMAs run under the first half's softmax
+      f32x16 spa[2], dpa[2];
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        f32x16 sp = {}, dp = {};
+        spa[b] = f32x16{};
+        dpa[b] = f32x16{};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          sp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(kt_s + koff[b][s]), qf[s], sp,
-                                                       0, 0, 0);
-          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(vt_s + koff[b][s]), df[s], dp,
-                                                       0, 0, 0);
+          spa[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(kt_s + koff[b][s]), qf[s],
+                                                           spa[b], 0, 0, 0);
+          dpa[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(vt_s + koff[b][s]), df[s],
+                                                           dpa[b], 0, 0, 0);
         }
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f32x16& sp = spa[b];
+        const f32x16& dp = dpa[b];
         // K^T fragments in flight under the softmax
         constexpr int KIMM = ST * STG;
         bf16x8 fq[2][2];
@@ -990,19 +1028,19 @@ __device__ __forceinline__ void dq_segment(char* smem, const bf16* qkv, int ld, 
 
 template <int QW, int KS, bool SK>
 __global__ __launch_bounds__(64 * QW * KS) __attribute__((amdgpu_waves_per_eu(2))) void attn_bwd_dq_kernel(
-    const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse, float* delta,
-    int T, int heads, bf16* dqkv, int ldd, AttnSK sk) {
+    const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse, float* ndel,
+    float* nl8, int T, int heads, bf16* dqkv, int ldd, AttnSK sk) {
   __shared__ __attribute__((aligned(16))) char smem[DqLds<QW, KS>::BYTES];
   const int ntk = (T + 63) / 64;
   if constexpr (!SK) {
-    dq_segment<QW, KS, false>(smem, qkv, ld, o, ldo, dout, lddo, lse, delta, T, heads, dqkv, ldd, blockIdx.x,
+    dq_segment<QW, KS, false>(smem, qkv, ld, o, ldo, dout, lddo, lse, ndel, nl8, T, heads, dqkv, ldd, blockIdx.x,
                               blockIdx.y, blockIdx.z, 0, ntk, sk, 0, 0);
   } else {
     const int nqb = (T + 32 * QW - 1) / (32 * QW);
     sk_walk(sk, ntk, [&](long bi, int t0, int cnt, int seg) {
       const int qbk = (int)(bi % nqb);
       const long nh = bi / nqb;
-      dq_segment<QW, KS, true>(smem, qkv, ld, o, ldo, dout, lddo, lse, delta, T, heads, dqkv, ldd, qbk,
+      dq_segment<QW, KS, true>(smem, qkv, ld, o, ldo, dout, lddo, lse, ndel, nl8, T, heads, dqkv, ldd, qbk,
                                (int)(nh % heads), (int)(nh / heads), t0, cnt, sk, bi, seg);
     });
   }
@@ -1055,20 +1093,22 @@ void launch_fwd(const bf16* qkv, int ld, int t, int heads, int nb, bf16* o, int 
   hipLaunchKernelGGL((attn_fwd_kernel<QW, KS>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, t, heads, o, ldo, lse);
 }
 
-// dQ first: it computes delta = rowsum(dO * O) for its resident queries and publishes it; dK/dV (next
-// launch, same stream) reads it -- no separate delta pass
+// dQ first: it computes delta = rowsum(dO * O) for its resident queries and publishes the dK/dV kernel's row
+// constants -delta (delta[0, nht)) and -8 lse (delta[nht, 2 nht)); dK/dV (next launch, same stream) reads them --
+// no separate delta pass
 template <int QW, int KS>
 void launch_bwd(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* dout, int lddo, const float* lse,
                 float* delta, int t, int heads, int nb, bf16* dqkv, int ldd, bool with_dq, bool with_dkdv,
                 hipStream_t st) {
   dim3 grid((t + 32 * QW - 1) / (32 * QW), heads, nb);
   const AttnSK none{};
+  float* nl8 = delta + (long)nb * heads * t;
   if (with_dq)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, o, ldo, dout,
-                       lddo, lse, delta, t, heads, dqkv, ldd, none);
+                       lddo, lse, delta, nl8, t, heads, dqkv, ldd, none);
   if (with_dkdv)
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<QW, KS, false>), grid, dim3(64 * QW * KS), 0, st, qkv, ld, dout, lddo,
-                       lse, delta, t, heads, dqkv, ldd, none);
+                       nl8, delta, t, heads, dqkv, ldd, none);
 }
 
 int device_cus() {
@@ -1114,12 +1154,13 @@ bool launch_bwd_sk(const bf16* qkv, int ld, const bf16* o, int ldo, const bf16* 
                    bool with_dq, bool with_dkdv, hipStream_t st) {
   AttnSK sk;
   if (!sk_plan(t, heads, nb, ws, ws_bytes, "DC_ATTN_SK", sk)) return false;
+  float* nl8 = delta + (long)nb * heads * t;
   if (with_dq)
     hipLaunchKernelGGL((attn_bwd_dq_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, o, ldo, dout,
-                       lddo, lse, delta, t, heads, dqkv, ldd, sk);
+                       lddo, lse, delta, nl8, t, heads, dqkv, ldd, sk);
   if (with_dkdv)
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<4, 1, true>), dim3((unsigned)sk.G), dim3(256), 0, st, qkv, ld, dout,
-                       lddo, lse, delta, t, heads, dqkv, ldd, sk);
+                       lddo, nl8, delta, t, heads, dqkv, ldd, sk);
   return true;
 }
 
@@ -1155,7 +1196,7 @@ extern "C" int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, cons
   const bf16* d = (const bf16*)dout;
   bf16* g = (bf16*)dqkv;
   const long wsb = ws_bytes < (1LL << 40) ? (long)ws_bytes : 0;
-  // dQ first (it publishes delta for dK/dV), then dK/dV: by the stream-K kernels where the plan applies, else on
+  // dQ first (it publishes the row constants for dK/dV), then dK/dV: by the stream-K kernels where the plan applies, else on
   // the plain grid
   if (!launch_bwd_sk(q, ld, ob, ldo, d, lddo, lse, delta_ws, t, heads, nb, g, ldd, ws, wsb, true, true, st)) {
     const int cfg = attn_cfg(t, heads, nb, true);

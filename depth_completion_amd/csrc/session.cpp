@@ -1101,7 +1101,7 @@ class UNetPlan {
     RB dout = grad_of.at(out.p);
     RB dr3 = buf(P, C), df = buf(P, 8 * C), dl3 = buf(P, C), dr1 = buf(P, C), dob = buf(P, C),
        dqkv = buf(P, 3 * C), dl1 = buf(P, C), dp = buf(P, C), dn0 = buf(P, C), dx = buf(P, C);
-    float* delta = fbuf((long)nb * H * T);
+    float* delta = fbuf(2L * nb * H * T);   // dc_attn_bwd's row constants (-delta, -8 lse)
     grad_of[x.p] = dx;
     auto e = extra_of.find(x.p);
     RB extra = e == extra_of.end() ? RB() : e->second;

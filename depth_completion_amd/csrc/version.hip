@@ -7,5 +7,5 @@
 #ifndef DC_BUILD_ID
 #define DC_BUILD_ID "unknown"
 #endif
-extern "C" int dc_abi_version(void) { return 20; }
+extern "C" int dc_abi_version(void) { return 21; }
 extern "C" const char* dc_build_id(void) { return DC_BUILD_ID; }

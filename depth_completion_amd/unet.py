@@ -595,7 +595,7 @@ class UNetPlan:
         dp = self.buf(P, C)
         dn0 = self.buf(P, C)
         dx = self.buf(P, C)
-        delta = self.fbuf(nb, H, T)
+        delta = self.fbuf(2, nb, H, T)   # the backward's row constants: -delta, -8 lse
         grad_of[id(x)] = dx
         extra = extra_of.get(id(x))
         st0, p, sl1, qkv, o, lse = d["st0"], d["p"], d["sl1"], d["qkv"], d["o"], d["lse"]

@@ -190,6 +190,8 @@ int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, const float*
  * (null: plain grid) */
 int dc_attn_fwd(const void* qkv, int ld, int nb, int t, int heads, void* o, int ldo, float* lse, float* ws,
                 long long ws_bytes, void* stream);
+/* delta_ws: fp32 scratch of 2 nb heads t floats (ABI 21; was nb heads t): the dQ kernel fills it with the dK/dV kernel's
+ * row constants, -rowsum(dO o O) then -8 lse */
 int dc_attn_bwd(const void* qkv, int ld, const void* o, int ldo, const void* dout, int lddo, const float* lse, int nb,
                 int t, int heads, float* delta_ws, void* dqkv, int ldd, float* ws, long long ws_bytes, void* stream);
 /* folded cross-attention on MFMA (csrc/crossattn.hip): U, D fp32 [heads][c] (dc_fold_cross_attention) are

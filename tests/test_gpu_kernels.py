@@ -430,7 +430,7 @@ def test_attention_fwd_bwd(ctx, n, t, heads, cfg, monkeypatch):
     lse = torch.empty(n, heads, t, device=dev)
     ops.attn_fwd(ctx, qkv_b, n, t, heads, ob, lse)
     dq = torch.empty_like(qkv_b)
-    delta = torch.empty(n, heads, t, device=dev)
+    delta = torch.empty(2, n, heads, t, device=dev)
     ops.attn_bwd(ctx, qkv_b, ob, do.to(torch.bfloat16).reshape(n * t, C), lse, n, t, heads, delta, dq)
     torch.cuda.synchronize()
     assert rel(ob.view(n, t, C), o) < 1e-2
@@ -489,7 +489,7 @@ def test_attention_bwd_stream_k(ctx, n, t, heads, monkeypatch):
     for mode in ("0", "2", "2b"):
         monkeypatch.setenv("DC_ATTN_SK", mode[0])
         dq = torch.zeros_like(qkv_b)
-        delta = torch.empty(n, heads, t, device=dev)
+        delta = torch.empty(2, n, heads, t, device=dev)
         ops.attn_bwd(ctx, qkv_b, ob, dob, lse, n, t, heads, delta, dq)
         torch.cuda.synchronize()
         outs[mode] = dq
@@ -833,8 +833,9 @@ def test_geglu_epilogues(ctx, algo, nsplit):
     assert rel(df.float(), ref) < 1e-2
 
 
+# (64, 300, 59, 1): a wide 320-column tile id, which would straddle geglu_n = 256 -- the library runs the 64 x 64 tile
 @pytest.mark.parametrize("c,rows,algo,nsplit", [(256, 300, 0, 0), (256, 300, 13, 2), (256, 300, 12, -1),
-                                                 (320, 6912, 0, 0)])
+                                                 (320, 6912, 0, 0), (64, 300, 59, 1)])
 def test_folded_ff2_proj_out(ctx, c, rows, algo, nsplit):
     """FF2 + proj_out folded into one linear over [gg | r2] (weights.FoldedPair, dc_fold_linear_pair): the forward
     (two sources, K = 5C) against the two linears in fp32, and the input-gradient with the GEGLU backward on the first

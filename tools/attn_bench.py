@@ -40,7 +40,7 @@ for n, t, heads in [(1, 6912, 5), (1, 1728, 10), (1, 432, 20), (1, 108, 20), (8,
     lse = torch.empty(n, heads, t, device=dev)
     do = torch.randn(n * t, C, device=dev).to(torch.bfloat16)
     dq = torch.empty_like(qkv)
-    delta = torch.empty(n, heads, t, device=dev)
+    delta = torch.empty(2, n, heads, t, device=dev)
     f = 4.0 * n * t * t * 64 * heads
     fw = [timed(lambda: ops.attn_fwd(ctx, qkv, n, t, heads, o, lse)) for _ in range(args.reps)]
     ms = min(fw)
