@@ -19,9 +19,11 @@ Also reported on the JSON line:
                  from the committed PMC passes over the graph-replayed step (profiles/pmc_step*.json, gfx950
                  corrections of MI355X_MICROARCH.md) for the latent shape they ran on;
                  `traffic_over_algorithmic` = those bytes over the launches' operands moved once (conv_bytes);
-                 `mfma_util` = the PMC MFMA-busy cycles over the graph-timed family time x 2.4 GHz x 1024 SIMDs
+                 `mfma_util` = the PMC MFMA-busy cycles over the graph-timed family time x 2.4 GHz x 1024 SIMDs,
+                 reported only when the record's conv_family_hash is this tree's (`pmc_current`)
   frame_roofline algorithmic TFLOP per frame (depth_completion_amd/flops.py, SURVEY §8d convention, at the
-                 run's own latent shape, steps and seeds) x fps / 2.5 PF
+                 run's own latent shape, steps and seeds) x fps / 2.5 PF; `executed_*`: the same less the decoder
+                 FLOPs the sparse-aware decode skips (its row-list launches against the dense decode)
   launches       kernel nodes of one captured guided step (hipGraphGetNodes)
   cpu_baseline   the oracle (CPU PyTorch restatement of the reference path, incl. weight-gradients as the
                  reference computes them) on this host's cores, rank 0 / N=1 only, on a bounded sample
@@ -89,10 +91,10 @@ def workload_name(h: int, w: int, batch: int, seeds: int) -> str:
     return "custom"
 
 
-def conv_flops(d) -> float:
+def conv_flops(d, dense: bool = False) -> float:
     """Algorithmic FLOPs of one dc_conv_gemm launch (real channels, valid taps only; a row-list launch
-    counts its rows, padding included)."""
-    M = d.nrows if d.rows else d.nb * d.hout * d.wout
+    counts its rows, padding included; dense: as if it ran on the whole map)."""
+    M = d.nrows if (d.rows and not dense) else d.nb * d.hout * d.wout
     K = d.kh * d.kw * d.cin
     f = 2.0 * M * d.cout * K
     if d.mode == 2:   # transposed stride-2 gather: on average 1/4 of the taps are valid
@@ -165,7 +167,9 @@ def measure_conv_kernel(pipe, st, reps: int = 3):
     finally:
         st["dec"].set_rows(None)
     flops = sum(conv_flops(d) for d in descs)
-    return n, max(t_all - t_rest, 1e-6), flops, nodes, sum(conv_bytes(d) for d in descs)
+    # the FLOPs the sparse-aware decode's row-list launches skip against the dense decode SURVEY §8d counts
+    skipped = sum(conv_flops(d, dense=True) - conv_flops(d) for d in descs if d.rows)
+    return n, max(t_all - t_rest, 1e-6), flops, nodes, sum(conv_bytes(d) for d in descs), skipped
 
 
 def graph_node_counts(raw_graph: int) -> dict:
@@ -476,7 +480,12 @@ def run_worker(args) -> None:
         del line["frame_roofline"]
     elif rank == 0:
         st = pipe._plans[(B * S, h, w)]
-        n_launch, conv_ms, conv_flops_, nodes, conv_bytes_ = measure_conv_kernel(pipe, st)
+        n_launch, conv_ms, conv_flops_, nodes, conv_bytes_, skipped = measure_conv_kernel(pipe, st)
+        # the frame's executed work: SURVEY's count less what the sparse-aware decode never computes (its row-list
+        # launches cover the resize taps' receptive fields only), so the sparse decode does not inflate the fraction
+        exec_tflop = (ff["per_frame"] - skipped * args.denoise_steps / B) / 1e12
+        line["frame_roofline"].update(executed_tflop_per_frame=round(exec_tflop, 2),
+                                      executed_frac_of_bf16_peak=round(fps_gpu * exec_tflop / PEAK_BF16_TFLOPS, 4))
         avg_ms = conv_ms / max(n_launch, 1)
         achieved = conv_flops_ / (conv_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",

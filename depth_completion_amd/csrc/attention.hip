@@ -352,10 +352,11 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
                                             float* lse, int qbk, int h, int n, int t0, int tcount) {
   constexpr int NT = 64 * QW;
   constexpr int S = FWD_S;
+  constexpr int STAGE = FwdLds<QW, KS>::STAGE;
   const int lane = threadIdx.x & 63, hh = lane >> 5;
   const int part = threadIdx.x / NT, wid = (threadIdx.x >> 6) - part * QW;
   const int lt = threadIdx.x - part * NT;
-  char* ring = smem + part * S * FwdLds<QW, KS>::STAGE;
+  char* ring = smem + part * S * STAGE;
   const int C = heads * 64;
   const bf16* base = qkv + (long)n * T * ld;
   const int my_q = qbk * (32 * QW) + wid * 32 + (lane & 31);
@@ -379,121 +380,138 @@ __device__ __forceinline__ void fwd_segment(char* smem, const bf16* qkv, int ld,
   TileDma<NT> dma;
   dma.init(lt, ld);
   auto issue = [&](int i) __attribute__((always_inline)) {
-    char* st = ring + (i % S) * FwdLds<QW, KS>::STAGE;
+    char* st = ring + (i % S) * STAGE;
     dma.issue(rk, st, (tb + i) * 64, T, ld, lt);
     dma.issue(rv, st + TILE_B, (tb + i) * 64, T, ld, lt);
   };
   constexpr int PER_TILE = 2 * TileDma<NT>::MIN_INSTR;  // LDS-DMA instructions per stage, every wave
-  int koff[2][4];
-  unsigned va[4][2][2];  // LDS addresses of the V^T pieces (the stage offset is an immediate)
+  // per-lane LDS offsets of the K rows and LDS addresses of the V^T pieces for key half b = 0 / k-slice s = 0: the
+  // swizzle phase depends on row bits 1..3 only, so key half b (+32 rows) and k-slice s (+16 rows) -- like the ring
+  // stage -- are immediate offsets (4096 b, 2048 s bytes), and only these 4 + 4 registers stay live
+  int koff[4];
+  unsigned va[2][2];
 #pragma unroll
-  for (int b = 0; b < 2; ++b)
+  for (int s = 0; s < 4; ++s) koff[s] = row_off(lane & 31, 2 * s + hh);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) koff[b][s] = row_off(32 * b + (lane & 31), 2 * s + hh);
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      const TrOff o = tr_off(16 * s, 32 * db, lane);
-      va[s][db][0] = lds_addr(ring) + o.lo;
-      va[s][db][1] = lds_addr(ring) + o.hi;
-    }
-  for (int i = 0; i < S - 1 && i < mine; ++i) issue(i);
-  // the ring stage is a compile-time constant in each copy of the body (ds_read immediate offsets)
-  auto step = [&](int i, auto STC) __attribute__((always_inline)) {
+  for (int db = 0; db < 2; ++db) {
+    const TrOff o = tr_off(0, 32 * db, lane);
+    va[db][0] = lds_addr(ring) + o.lo;
+    va[db][1] = lds_addr(ring) + o.hi;
+  }
+  for (int i = 0; i < 2 && i < mine; ++i) issue(i);   // the DMA runs two tiles ahead
+  f32x16 sacc[2];
+  // S = K Q^T of tile i (ring stage ST: compile-time, the ds_read offsets are immediates)
+  auto phase_s = [&](auto STC) __attribute__((always_inline)) {
     constexpr int ST = decltype(STC)::value;
-    if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();  // S = 3: at most one younger tile in flight
-    else vm_wait_n<0>();
-    ring_barrier();
-    if (i + S - 1 < mine) issue(i + S - 1);
-    if (i < mine) {
-      const int kt = tb + i;
-      const char* kt_s = ring + ST * FwdLds<QW, KS>::STAGE;
-      const char* vt_s = kt_s + TILE_B;
-      f32x16 sacc[2];
+    const char* kt_s = ring + ST * STAGE;
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < 2; ++b) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
+      for (int r = 0; r < 16; ++r) sacc[b][r] = 0.0f;
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-          sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              *reinterpret_cast<const bf16x8*>(kt_s + koff[b][s]), qf[s], sacc[b], 0, 0, 0);
-      }
-      // online softmax in raw score units; exp2 with log2(e) folded into one FMA per score;
-      // keys beyond T exist only in the last tile; O is rescaled only when some row max grew
-      if ((kt + 1) * 64 > T) {
-        asm volatile("" ::: "memory");  // keep this a branch: if-converted it costs ~60 VALU per tile
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (key >= T) sacc[b][r] = -INFINITY;
-          }
-      }
-      // row max: four independent v_max3 chains over the lane's 32 scores (raw v_max3: no canonicalising fmaxf on
-      // the MFMA results, and no 32-deep serial chain), then the row's other lane half by v_permlane32_swap
-      float mc[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const int b = c >> 1, r0 = 8 * (c & 1);
-        float t = max3_raw(sacc[b][r0], sacc[b][r0 + 1], sacc[b][r0 + 2]);
-        t = max3_raw(t, sacc[b][r0 + 3], sacc[b][r0 + 4]);
-        t = max3_raw(t, sacc[b][r0 + 5], sacc[b][r0 + 6]);
-        mc[c] = max3_raw(t, sacc[b][r0 + 7], sacc[b][r0 + 7]);
-      }
-      const float mx = rowmax_pair(max3_raw(max3_raw(mc[0], mc[1], mc[2]), mc[3], mc[3]));
-      // lazy rescale: the reference max moves only when a row max exceeds it by more than FWD_TAU, so
-      // weights stay <= e^FWD_TAU (exact in fp32 / bf16 relative terms; O and l share the reference)
-      if (__any(mx > m + FWD_TAU)) {
-        const float mnew = fmaxf(m, mx);
-        const float alpha = fast_exp2((m - mnew) * LOG2E);
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
-        l *= alpha;
-        m = mnew;
-      }
-      // row sums in fp32 from the unrounded weights: the LSE the backward recomputes P from must not carry
-      // P's bf16 rounding (a sum of bf16 P, e.g. on the MFMA pipe, is off by up to ~4e-3 in the LSE on
-      // peaked rows and biases the guidance gradient: tools/attn_acc.py, profiles/r02m)
-      // (four partial sums: independent add chains, summed in a fixed order)
-      const float ml = m * LOG2E;
-      float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int s = 0; s < 4; ++s)
+        sacc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            *reinterpret_cast<const bf16x8*>(kt_s + 4096 * b + koff[s]), qf[s], sacc[b], 0, 0, 0);
+    }
+  };
+  // online softmax of tile i (in sacc): updates (m, l), rescales O when the reference max moves, and returns P as the
+  // four bf16 B-operand fragments of the P.V product
+  auto phase_sm = [&](int i, bf16x8 (&pf)[4]) __attribute__((always_inline)) {
+    const int kt = tb + i;
+    // online softmax in raw score units; exp2 with log2(e) folded into one FMA per score;
+    // keys beyond T exist only in the last tile; O is rescaled only when some row max grew
+    if ((kt + 1) * 64 > T) {
+      asm volatile("" ::: "memory");  // keep this a branch: if-converted it costs ~60 VALU per tile
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
-          sacc[b][r] = pv;
-          ps[r & 3] += pv;
+          const int key = kt * 64 + 32 * b + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (key >= T) sacc[b][r] = -INFINITY;
         }
-      l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
-      // V^T fragments: two k-slices in flight ahead of the MFMAs that consume them
-      constexpr int VIMM = ST * FwdLds<QW, KS>::STAGE + TILE_B;
-      bf16x8 vf[4][2];
+    }
+    // row max: four independent v_max3 chains over the lane's 32 scores (raw v_max3: no canonicalising fmaxf on
+    // the MFMA results, and no 32-deep serial chain), then the row's other lane half by v_permlane32_swap
+    float mc[4];
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+    for (int c = 0; c < 4; ++c) {
+      const int b = c >> 1, r0 = 8 * (c & 1);
+      float t = max3_raw(sacc[b][r0], sacc[b][r0 + 1], sacc[b][r0 + 2]);
+      t = max3_raw(t, sacc[b][r0 + 3], sacc[b][r0 + 4]);
+      t = max3_raw(t, sacc[b][r0 + 5], sacc[b][r0 + 6]);
+      mc[c] = max3_raw(t, sacc[b][r0 + 7], sacc[b][r0 + 7]);
+    }
+    const float mx = rowmax_pair(max3_raw(max3_raw(mc[0], mc[1], mc[2]), mc[3], mc[3]));
+    // lazy rescale: the reference max moves only when a row max exceeds it by more than FWD_TAU, so
+    // weights stay <= e^FWD_TAU (exact in fp32 / bf16 relative terms; O and l share the reference)
+    if (__any(mx > m + FWD_TAU)) {
+      const float mnew = fmaxf(m, mx);
+      const float alpha = fast_exp2((m - mnew) * LOG2E);
 #pragma unroll
-        for (int db = 0; db < 2; ++db) vf[s][db] = trans_frag_nw<VIMM>(va[s][db][0], va[s][db][1]);
+      for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        if (s + 2 < 4) {
+        for (int r = 0; r < 16; ++r) oacc[db][r] *= alpha;
+      l *= alpha;
+      m = mnew;
+    }
+    // row sums in fp32 from the unrounded weights: the LSE the backward recomputes P from must not carry
+    // P's bf16 rounding (a sum of bf16 P, e.g. on the MFMA pipe, is off by up to ~4e-3 in the LSE on
+    // peaked rows and biases the guidance gradient: tools/attn_acc.py, profiles/r02m)
+    // (four partial sums: independent add chains, summed in a fixed order)
+    const float ml = m * LOG2E;
+    float ps[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int db = 0; db < 2; ++db) vf[s + 2][db] = trans_frag_nw<VIMM>(va[s + 2][db][0], va[s + 2][db][1]);
-          lgkm_wait<8>(vf[s][0], vf[s][1]);
-        } else if (s == 2) {
-          lgkm_wait<4>(vf[s][0], vf[s][1]);
-        } else {
-          lgkm_wait<0>(vf[s][0], vf[s][1]);
-        }
-        const bf16x8 pf = acc_to_frag(sacc[s >> 1], s & 1);
+    for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int db = 0; db < 2; ++db)
-          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], pf, oacc[db], 0, 0, 0);
+      for (int r = 0; r < 16; ++r) {
+        const float pv = fast_exp2(fmaf(sacc[b][r], LOG2E, -ml));
+        sacc[b][r] = pv;
+        ps[r & 3] += pv;
       }
+    l += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) pf[s] = acc_to_frag(sacc[s >> 1], s & 1);
+  };
+  // O += P V, V^T fragments of ring stage ST: two k-slices in flight ahead of the MFMAs that consume them
+  auto phase_pv = [&](const bf16x8 (&pf)[4], auto STC) __attribute__((always_inline)) {
+    constexpr int ST = decltype(STC)::value;
+    constexpr int VIMM = ST * STAGE + TILE_B;
+    bf16x8 vf[4][2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db) vf[0][db] = trans_frag_nw<VIMM>(va[db][0], va[db][1]);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) vf[1][db] = trans_frag_nw<VIMM + 2048>(va[db][0], va[db][1]);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s == 0) {
+#pragma unroll
+        for (int db = 0; db < 2; ++db) vf[2][db] = trans_frag_nw<VIMM + 2 * 2048>(va[db][0], va[db][1]);
+        lgkm_wait<8>(vf[s][0], vf[s][1]);
+      } else if (s == 1) {
+#pragma unroll
+        for (int db = 0; db < 2; ++db) vf[3][db] = trans_frag_nw<VIMM + 3 * 2048>(va[db][0], va[db][1]);
+        lgkm_wait<8>(vf[s][0], vf[s][1]);
+      } else if (s == 2) {
+        lgkm_wait<4>(vf[s][0], vf[s][1]);
+      } else {
+        lgkm_wait<0>(vf[s][0], vf[s][1]);
+      }
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+        oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[s][db], pf[s], oacc[db], 0, 0, 0);
+    }
+  };
+  // one tile step (ring stage ST: compile-time)
+  auto step = [&](int i, auto STC) __attribute__((always_inline)) {
+    if (mine - 1 - i >= 1) vm_wait_n<PER_TILE>();  // at most one younger tile in flight
+    else vm_wait_n<0>();
+    ring_barrier();
+    if (i + 2 < mine) issue(i + 2);
+    if (i < mine) {
+      phase_s(STC);
+      bf16x8 pf[4];
+      phase_sm(i, pf);
+      phase_pv(pf, STC);
     }
   };
   static_assert(S == 3, "the unrolled ring below assumes three stages");
@@ -1073,6 +1091,10 @@ int attn_cfg(int t, int heads, int nb, bool bwd) {
   // blocks of (4, 2) over the same key tiles -- measured 22.1 vs 26.2 us at T = 432 (profiles/r05aa/); the model
   // below does not see it (it prices resident waves, not the sequential key-tile chain of a small grid)
   if (bwd && (long)t * nb <= 512) return 2;
+  // many blocks (batch 8 / the C5 ensemble): the forward's (4, 1) -- three 4-wave blocks per CU -- beats the 10-wave
+  // key-split blocks the model below prefers (L0 batch 8 605 vs 653 us, L2 batch 8 23.9 vs 26.3 us; batch 1, where
+  // (4, 1) leaves one block per CU, keeps (5, 2): 104 vs 142 us; profiles/r06d/)
+  if (!bwd && (long)((t + 127) / 128) * heads * nb > 2L * 256) return 0;
   int best = 0;
   double best_t = 1e30;
   for (int i = 0; i < ncfg; ++i) {

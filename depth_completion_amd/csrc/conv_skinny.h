@@ -92,6 +92,7 @@ struct SkinnyBlock {
     const int soff = (T * p.cin + (cg + J) * 64 + H * 32) * 2;
 #pragma unroll
     for (int jj = 0; jj < NJ; ++jj) {
+      // default cache policy: nt (aux 2) measured 2.2 % slower at C2 (profiles/r06b/)
       const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rb, wv[jj], soff, 0);
       wr[S][jj] = __builtin_bit_cast(bf16x8, v);
     }

@@ -195,7 +195,11 @@ def test_c2_full_unet_50_steps(full_c2):
     # every latent by +-lr on the sign of a gradient near zero); per step the HIP path is as close to the fp32
     # oracle as the bf16 oracle is (test_c2_teacher_forced_per_step).  Bounds: relative to that drift, and the
     # stated absolute C2 tolerance -- fitted per-pixel |depth diff| <= 5 % mean / 19 % p99 of the frame's depth
-    # range (measured HIP 3.91 % / 14.8 %, profiles/r03b/; ~28 % headroom)
+    # range (measured HIP 3.91 % / 14.8 %, profiles/r03b/; ~28 % headroom).  Why 10x SURVEY's proposed 0.5 % / 2 %:
+    # that figure is below the reference path's own bf16-vs-fp32 drift at this workload (the bf16 oracle is 3.86 % /
+    # 14.5 % from the fp32 oracle after 50 guided steps), so no bf16 implementation -- the reference's included --
+    # can meet it end to end; the absolute bound sits ~1.3x above that drift, and the per-step bound (each step from
+    # the fp32 oracle's state, within 1.25x the bf16 oracle's own per-step error) is test_c2_teacher_forced_per_step
     assert mean_h <= 2 * mean_b + 1e-3 and p99_h <= 2 * p99_b + 1e-3
     assert mean_h <= 0.05 and p99_h <= 0.19
     assert lat_h <= 2 * lat_b + 2e-3
@@ -418,9 +422,9 @@ def test_c4_full_unet_50_steps():
     assert mean_h <= 0.035 and p99_h <= 0.13
 
 
-def test_c5_full_unet_ensemble_3_steps():
+def test_c5_full_unet_ensemble_10_steps():
     """C5 (nuScenes 1600x900 at resolution 768: latent 54x96, 3000 points) with the 10-seed ensemble as ONE
-    batch-10 call through the FULL Marigold v1-0 UNet, 3 guided steps, then mean + compute_affine_params
+    batch-10 call through the FULL Marigold v1-0 UNet, 10 guided steps, then mean + compute_affine_params
     (marigold_dc.py:53-128), against the oracle's per-seed loop.  Bound: 2x the bf16 oracle's own error + 2e-3
     of the range (mean |d|), and per seed the latent within 2x the bf16 oracle's latent error + 2e-3."""
     from depth_completion_amd.config import MARIGOLD_V1
@@ -429,7 +433,7 @@ def test_c5_full_unet_ensemble_3_steps():
     imgs, sparses = synth_inputs(1, h, w, 3000, seed=50)
     seeds = list(range(2024, 2034))
     noises = [_noise(sd, 54, 96) for sd in seeds]
-    kw = dict(norm="const", steps=3, resolution=768)
+    kw = dict(norm="const", steps=10, resolution=768)
     lat32, lat16 = [], []
     o32, usd, vsd, emb = build(UNetConfig(), MARIGOLD_V1, torch.float32, dev)
     r32, *_ = P.ensemble(_LatCollect(o32, lat32), imgs.to(dev), sparses.to(dev), 120.0, noises, **kw)
@@ -448,7 +452,7 @@ def test_c5_full_unet_ensemble_3_steps():
     err_b = float((r16.cpu() - r32.cpu()).abs().mean()) / rng
     p99_h = float(torch.quantile(((dh.cpu() - r32.cpu()).abs() / rng).flatten()[::7], 0.99))
     lat_e = [(_lat_err(lat[k:k + 1], lat32[k]), _lat_err(lat16[k], lat32[k])) for k in range(10)]
-    print(f"\nC5 10-seed ensemble (full UNet, 1600x900, 3000 pts, 3 steps): HIP |d| mean {err_h:.5f} p99 {p99_h:.5f} "
+    print(f"\nC5 10-seed ensemble (full UNet, 1600x900, 3000 pts, 10 steps): HIP |d| mean {err_h:.5f} p99 {p99_h:.5f} "
           f"of range | oracle-bf16 {err_b:.5f}; per-seed latent HIP/bf16 "
           + " ".join(f"{a:.4f}/{b:.4f}" for a, b in lat_e))
     assert err_h <= 2 * err_b + 2e-3
