@@ -404,7 +404,7 @@ class MarigoldDepthCompletionPipeline:
         if self.use_graph:
             g = st["graph"]
             gkey = (guided, guided and cf, opt_code, kld_code, float(kld_weight), steps, H, W, RH, RW, lr_latent,
-                    lr_scaling, loss_flags if full_loss else 0, row_counts, self._scheduler_key())
+                    lr_scaling, loss_flags if full_loss else 0, self._scheduler_key(), row_counts)
             if g is None or st["graph_key"] != gkey:
                 # (re)capture: the graph binds this call's tables -- the plan's persistent guide buffers for (n, H, W)
                 # and the kept (steps, lr, optimiser) tables, which later calls with the same key rewrite in place

@@ -70,20 +70,26 @@ def test_cli_default_mode_matches_oracle(tmp_path, monkeypatch):
     r = CliRunner().invoke(main, [str(tmp_path / "data"), str(out), "--synthetic-weights", "0", "--unet-config",
                                   "tiny", "--res", "64", "--steps", "3", "--compress", "npy", "--vis", "False"])
     assert r.exit_code == 0, (r.output, r.exception)
-    assert len(calls) == 1
-    imgs, sps, max_depth, kw, lshape = calls[0]
+    assert len(calls) >= 1 and sum(c[0].shape[0] for c in calls) == 2   # the CLI's batches cover both frames
     dense = torch.stack([torch.from_numpy(np.load(p)) for p in sorted((out / "dense" / "cam0").glob("*.npy"))])
     assert dense.shape == (2, 1, 48, 64)
-    # the pipeline's default initial noise: CPU torch.Generator(seed), [1, 4, h, w] bf16 (deviation 1)
-    noise = torch.randn((1, 4, lshape[-2], lshape[-1]), generator=torch.Generator().manual_seed(kw.get("seed", 2024)),
-                        dtype=torch.bfloat16)
-    res = {}
-    for dt in (torch.float32, torch.bfloat16):
-        o, *_ = build(tiny_unet_config(), TINY, dt, ORACLE)
-        res[dt], _ = o(imgs.to(ORACLE), sps.to(ORACLE), max_depth, init_noise=noise, **kw)
-    mean_h, p99_h = fitted_error(dense, res[torch.float32], sps)
-    mean_b, p99_b = fitted_error(res[torch.bfloat16], res[torch.float32], sps)
-    print(f"\nCLI default mode (tiny UNet, 2 frames, 3 steps): written dense fitted |d| mean {mean_h:.5f} p99 {p99_h:.5f}"
-          f" | oracle-bf16 mean {mean_b:.5f} p99 {p99_b:.5f}; call kwargs {sorted(kw)}")
+    oracles = {dt: build(tiny_unet_config(), TINY, dt, ORACLE)[0] for dt in (torch.float32, torch.bfloat16)}
+    res = {torch.float32: [], torch.bfloat16: []}
+    sps_all = []
+    for imgs, sps, max_depth, kw, lshape in calls:
+        assert kw.get("pred_latents_prev") is None   # (no --use-prev-latent: every call starts from its noise)
+        # the pipeline's default initial noise: CPU torch.Generator(seed), [1, 4, h, w] bf16 (deviation 1)
+        noise = torch.randn((1, 4, lshape[-2], lshape[-1]),
+                            generator=torch.Generator().manual_seed(kw.get("seed", 2024)), dtype=torch.bfloat16)
+        for dt, o in oracles.items():
+            d, _ = o(imgs.to(ORACLE), sps.to(ORACLE), max_depth, init_noise=noise, **kw)
+            res[dt].append(d.cpu())
+        sps_all.append(sps)
+    sps = torch.cat(sps_all)
+    d32, d16 = torch.cat(res[torch.float32]), torch.cat(res[torch.bfloat16])
+    mean_h, p99_h = fitted_error(dense, d32, sps)
+    mean_b, p99_b = fitted_error(d16, d32, sps)
+    print(f"\nCLI default mode (tiny UNet, 2 frames, 3 steps, {len(calls)} calls): written dense fitted |d| mean "
+          f"{mean_h:.5f} p99 {p99_h:.5f} | oracle-bf16 mean {mean_b:.5f} p99 {p99_b:.5f}; call kwargs {sorted(calls[0][3])}")
     assert mean_h <= 2 * mean_b + 1e-3 and p99_h <= 2 * p99_b + 1e-3
     assert mean_h <= 0.02 and p99_h <= 0.08
