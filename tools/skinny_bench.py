@@ -5,7 +5,8 @@ Cache), so the weights stream from HBM as they do in the sampler step, where eac
 per pass.  For each shape: the committed table's (algo, split), then every skinny algo x split; the output's
 relative error against the tuned launch is a quick correctness screen (tests/test_gpu_kernels.py has the real tests).
 Reports us per launch, TF/s and the weight-stream rate (weight bytes / time).
-Usage: python tools/skinny_bench.py [--reps 20] [--set l2|l3|taesd|all] [--algos 43 44 ...]
+Usage: python tools/skinny_bench.py [--reps 20] [--set l2|l3|taesd|all] [--algos 43 44 ...] [--copies N] [--tuned-only]
+(--copies N: rotate N weight copies instead -- 1 or 2 leave the weights in the Infinity Cache: warm against cold)
 (taesd: the 64-channel decoder convs, for the weight-resident persistent variants, algo ids 55..)
 """
 import argparse
@@ -63,6 +64,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--set", default="all")
     ap.add_argument("--algos", type=int, nargs="*")
+    ap.add_argument("--copies", type=int, default=0)
+    ap.add_argument("--tuned-only", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     ctx = Ctx(dev)
@@ -79,7 +82,7 @@ def main():
             kk, pad = 3, 1
         ktot = kk * kk * cin
         wbytes = cout * ktot * 2
-        ncopy = max(2, min(args.reps, math.ceil(600e6 / wbytes)))
+        ncopy = args.copies or max(2, min(args.reps, math.ceil(600e6 / wbytes)))
         x = torch.randn(nb * hin * win, cin, device=dev).to(torch.bfloat16)
         ws = [(torch.randn(cout, ktot, device=dev) / math.sqrt(ktot)).to(torch.bfloat16) for _ in range(ncopy)]
         b = torch.randn(cout, device=dev)
@@ -104,7 +107,7 @@ def main():
         print(f"{name:32s} tuned {tuned}: {t0:7.1f} us  {flops / t0 / 1e6:6.1f} TF/s  {wbytes / t0 / 1e3:7.1f} GB/s",
               flush=True)
         best = (t0, tuned)
-        for a in algos:
+        for a in ([] if args.tuned_only else algos):
             for s in (1, 2, 3, 4, 5, 6, 8, 10, 12, 16, 20, -4, -6, -8, -10, -12, -16, -20):
                 try:
                     ds = descs(a, s)
