@@ -1068,7 +1068,16 @@ class UNetPlan {
     Exec& ex = ex_;
     auto f2 = gn_bwd_fuse(h1, hh * ww, cout, r->n2, true, st2);
     auto f1 = gn_bwd_fuse(x, hh * ww, cin, r->n1, true, st1, x2, c1);
+    // the shortcut's input-gradient into its own buffer, added by the GroupNorm backward (as unet.py, which runs it
+    // as a concurrent graph branch)
+    RB dsc = r->has_sc ? buf(P, cin) : RB();
     bwd_.push_back([=, &ex]() {
+      if (r->has_sc) {
+        Exec::Conv s;
+        s.x = dout; s.nb = nb; s.hin = hh; s.win = ww; s.cin = cout; s.hout = hh; s.wout = ww; s.cout = cin;
+        s.kh = 1; s.kw = 1; s.pad = 0; s.w = r->sc.wd; s.ktot = r->sc.ktot_d; s.y = dsc;
+        ex.conv(s);
+      }
       Exec::Conv a;
       a.x = dout; a.nb = nb; a.hin = hh; a.win = ww; a.cin = cout; a.hout = hh; a.wout = ww; a.cout = cout;
       a.w = r->c2.wd; a.ktot = r->c2.ktot_d; a.y = dg2;
@@ -1080,15 +1089,7 @@ class UNetPlan {
       b.w = r->c1.wd; b.ktot = r->c1.ktot_d; b.y = dg1;
       b.gn = f1.second;
       ex.conv(b);
-      if (!r->has_sc) {
-        gn_bwd(x, hh * ww, cin, r->n1, true, st1, f1.first, dg1, dx, x2, c1, dout, extra);
-      } else {
-        gn_bwd(x, hh * ww, cin, r->n1, true, st1, f1.first, dg1, dx, x2, c1, extra);
-        Exec::Conv s;
-        s.x = dout; s.nb = nb; s.hin = hh; s.win = ww; s.cin = cout; s.hout = hh; s.wout = ww; s.cout = cin;
-        s.kh = 1; s.kw = 1; s.pad = 0; s.w = r->sc.wd; s.ktot = r->sc.ktot_d; s.resid = dx; s.y = dx;
-        ex.conv(s);
-      }
+      gn_bwd(x, hh * ww, cin, r->n1, true, st1, f1.first, dg1, dx, x2, c1, r->has_sc ? dsc : dout, extra);
     });
   }
 

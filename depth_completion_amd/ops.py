@@ -103,6 +103,18 @@ class Ctx:
             self._picked[key] = pick_variant(self._table, key)
         return self._picked[key]
 
+    def side(self) -> "Ctx":
+        """A context for a concurrent graph branch: its own stream (``side_stream``) and its own workspace (split-K
+        partials and tile counters must not be shared with the main stream's launches), the same variant tables."""
+        s = self.__dict__.get("_side")
+        if s is None:
+            s = object.__new__(Ctx)
+            s.__dict__.update(self.__dict__)
+            s.ws = torch.zeros_like(self.ws)
+            s.side_stream = torch.cuda.Stream(self.device)
+            self._side = s
+        return s
+
     @property
     def stream(self) -> int:
         if self.device.type != "cuda":

@@ -215,6 +215,12 @@ class UNetPlan:
         self._gn_next = 0
         self._gn_targets: dict = {}   # id(tensor) -> [(acc, coff, groups, cpg, hw)]
         self._gn_fuse: dict = {}      # id(tensor) -> ops.GnFuse, built at the first call
+        # the resnet shortcut convs (forward 1x1 and its input-gradient) depend on nothing of their block's main branch
+        # (GN -> conv -> GN -> conv).  DC_SIDE_STREAM=1 runs them on a second stream, a fork / join in the captured
+        # step graph, to fill CUs the main branch leaves idle at the small levels; measured 5 % slower at C2 (1.733 ->
+        # 1.645 fps, ~22 us per fork / join: the graph's cross-queue waits cost more than the overlap returns,
+        # profiles/r06p), so one stream is the default.  Same arithmetic either way.
+        self.side = ctx.side() if dev.type == "cuda" and os.environ.get("DC_SIDE_STREAM", "0") == "1" else None
         self._build_forward()
         self.bwd: list = []
         self._build_backward()
@@ -229,6 +235,19 @@ class UNetPlan:
         t = torch.zeros(*shape, dtype=torch.float32, device=self.dev)
         self.saved.append(t)
         return t
+
+    def _branch(self, fn):
+        """fn(ctx) as a branch forked from the current stream (on the side context's stream and workspace); returns
+        the join, to be called before the first consumer of the branch's output."""
+        if self.side is None:
+            fn(self.ctx)
+            return lambda: None
+        main = torch.cuda.current_stream(self.dev)
+        ss = self.side.side_stream
+        ss.wait_stream(main)
+        with torch.cuda.stream(ss):
+            fn(self.side)
+        return lambda: main.wait_stream(ss)
 
     # ------------------------------------------------------------------ fused GroupNorm statistics
     def _gn_acc(self) -> torch.Tensor:
@@ -313,14 +332,18 @@ class UNetPlan:
         acc2 = self._gn_consumer(h1, cout, hh * ww)
 
         def f():
+            join = None
+            if r.shortcut is not None:
+                join = self._branch(lambda c: ops.conv_gemm(
+                    c, x, r.shortcut.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout, kh=1, kw=1,
+                    pad=0, x2=x2, c1=c1, bias=r.shortcut.bias, y=sc))
             self._gn_fwd(x, hh * ww, cin, r.norm1, True, acc1, g1, st1, x2=x2, c1=c1)
             self._conv_fwd(g1, r.conv1.wf, h1, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
                            bias=r.conv1.bias, rowbias=r.temb_table, rowbias_ld=cout)
             self._gn_fwd(h1, hh * ww, cout, r.norm2, True, acc2, g2, st2)
             res = x
-            if r.shortcut is not None:
-                ops.conv_gemm(ctx, x, r.shortcut.wf, nb=nb, hin=hh, win=ww, cin=cin, hout=hh, wout=ww, cout=cout,
-                              kh=1, kw=1, pad=0, x2=x2, c1=c1, bias=r.shortcut.bias, y=sc)
+            if join is not None:
+                join()
                 res = sc
             self._conv_fwd(g2, r.conv2.wf, out, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout,
                            bias=r.conv2.bias, resid=res)
@@ -559,19 +582,25 @@ class UNetPlan:
 
         acc2, gn2 = self._gn_bwd_fuse(h1, hh * ww, cout, r.norm2, True, st2)
         acc1, gn1 = self._gn_bwd_fuse(x, hh * ww, cin, r.norm1, True, st1, x2=x2, c1=c1)
+        # the shortcut's input-gradient (a side branch, _branch) lands in its own buffer and enters dx as the
+        # GroupNorm backward's first addend, where the identity shortcut's dout goes
+        dsc = self.buf(P, cin) if r.shortcut is not None else None
 
         def b():
+            join = None
+            if r.shortcut is not None:
+                join = self._branch(lambda c: ops.conv_gemm(
+                    c, dout, r.shortcut.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin, kh=1, kw=1,
+                    pad=0, y=dsc))
             ops.conv_gemm(ctx, dout, r.conv2.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cout, y=dg2,
                           gn=gn2)
             self._gn_bwd(h1, hh * ww, cout, r.norm2, True, st2, acc2, dg2, dh1)
             ops.conv_gemm(ctx, dh1, r.conv1.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin, y=dg1,
                           gn=gn1)
-            if r.shortcut is None:
-                self._gn_bwd(x, hh * ww, cin, r.norm1, True, st1, acc1, dg1, dx, x2=x2, c1=c1, add1=dout, add2=extra)
-            else:
-                self._gn_bwd(x, hh * ww, cin, r.norm1, True, st1, acc1, dg1, dx, x2=x2, c1=c1, add1=extra)
-                ops.conv_gemm(ctx, dout, r.shortcut.wd, nb=nb, hin=hh, win=ww, cin=cout, hout=hh, wout=ww, cout=cin,
-                              kh=1, kw=1, pad=0, resid=dx, y=dx)
+            if join is not None:
+                join()
+            self._gn_bwd(x, hh * ww, cin, r.norm1, True, st1, acc1, dg1, dx, x2=x2, c1=c1,
+                         add1=dout if dsc is None else dsc, add2=extra)
 
         return b
 
