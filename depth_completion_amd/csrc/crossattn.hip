@@ -33,8 +33,10 @@ constexpr int kRows = 16;      // rows per block (one MFMA M tile)
 //   NW  8: <= 2 channel chunks, <= 3 column tiles -> C <= 384  (UNet level 0: 320)
 //   NW 16: <= 3 channel chunks, <= 5 column tiles -> C <= 1280 (levels 1-3: 640, 1280)
 template <int NW> struct Fit;
-template <> struct Fit<8> { static constexpr int MK = 2, MCT = 3; };
-template <> struct Fit<16> { static constexpr int MK = 3, MCT = 5; };
+template <> struct Fit<8> { static constexpr int MK = 2, MCT = 3, MAXC = 384; };
+template <> struct Fit<16> { static constexpr int MK = 3, MCT = 5, MAXC = 1280; };
+// per-channel vectors (gamma, beta, c0) staged in LDS: elements per thread of the block-cooperative load
+template <int NW> constexpr int kStage = (Fit<NW>::MAXC + 64 * NW - 1) / (64 * NW);
 constexpr int kMaxC = 1280;
 
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -144,7 +146,10 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, 
   __shared__ float s_part[NW][kRows][kHP + 1];
   __shared__ float s_sig[kRows][kHP + 4];
   __shared__ float s_tile[NW][kRows][17];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  // gamma, beta, c0 staged once per block: read from global memory inside the phases below they were dependent
+  // round trips, one per channel chunk (gamma, beta) and one per column tile (c0)
+  __shared__ float s_aff[3][Fit<NW>::MAXC];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const long row0 = (long)blockIdx.x * kRows;
   const long row = row0 + r;
   const bool ok = row < rows;
@@ -156,25 +161,40 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, 
 
   // phase 1: x chunks and the logits tables in flight together; LayerNorm statistics (two-pass, fp32, the
   // waves' partials folded in wave order)
+  // every load unconditional (a row past the end reads the last row; nothing of it is stored): a load guarded by a
+  // lane condition sits in a divergent branch, and the compiler waits for it before leaving the branch
+  const long rowc = ok ? row : rows - 1;
+  // (chunks past the wave's last re-read it and are skipped at every use)
   bf16x8 xv[MK];
 #pragma unroll
-  for (int i = 0; i < MK; ++i) {
-    if (kb + i < ke && ok) {
-      xv[i] = ld8(x + row * ldx + (kb + i) * 32 + g * 8);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) xv[i][j] = (bf16)0.0f;
-    }
-  }
+  for (int i = 0; i < MK; ++i) xv[i] = ld8(x + rowc * ldx + min(kb + i, ke - 1) * 32 + g * 8);
   bf16x8 bk[MK][2][2];
   load_k<MK>(kb, ke, T.uh, T.ul, c, r, g, bk);
+  float aff[3][kStage<NW>];
+#pragma unroll
+  for (int k = 0; k < kStage<NW>; ++k) {
+    const int i = min((int)threadIdx.x + 64 * NW * k, c - 1);
+    aff[0][k] = gamma[i];
+    aff[1][k] = beta[i];
+    aff[2][k] = c0[i];
+  }
   float s = 0.0f;
 #pragma unroll
   for (int i = 0; i < MK; ++i)
+    if (kb + i < ke)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += (float)xv[i][j];
+      for (int j = 0; j < 8; ++j) s += (float)xv[i][j];
   s = rowsum4(s);
   if (g == 0) s_red[w][r] = s;
+#pragma unroll
+  for (int k = 0; k < kStage<NW>; ++k) {
+    const int i = threadIdx.x + 64 * NW * k;
+    if (i < c) {
+      s_aff[0][i] = aff[0][k];
+      s_aff[1][i] = aff[1][k];
+      s_aff[2][i] = aff[2][k];
+    }
+  }
   __syncthreads();
   float tot = 0.0f;
 #pragma unroll
@@ -203,7 +223,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, 
     if (kb + i < ke) {
       const int ch = (kb + i) * 32 + g * 8;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) xv[i][j] = (bf16)(((float)xv[i][j] - mu) * rs * gamma[ch + j] + beta[ch + j]);
+      for (int j = 0; j < 8; ++j) xv[i][j] = (bf16)(((float)xv[i][j] - mu) * rs * s_aff[0][ch + j] + s_aff[1][ch + j]);
     }
   }
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -253,7 +273,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, 
       o = mfma(sh, bt[t][0], o);
       o = mfma(sh, bt[t][1], o);
       o = mfma(sl, bt[t][0], o);
-      const float cv = c0[ct * 16 + r];
+      const float cv = s_aff[2][ct * 16 + r];
 #pragma unroll
       for (int e = 0; e < 4; ++e) s_tile[w][g * 4 + e][r] = (float)(bf16)(o[e] + cv);
       __builtin_amdgcn_wave_barrier();
@@ -328,19 +348,26 @@ template <int MAXV>
 __device__ __forceinline__ void ln3_bwd_row(const Ln3Bwd& L, long row, int c, int lane, bf16* out) {
   const int nv = c >> 3;
   const float mu = L.stats3[row * 2], rs = L.stats3[row * 2 + 1];
+  // the row's loads all issued up front, the residual addend included (clamped segments, skipped below): read after
+  // the row sums, the addend was a second dependent round trip
+  bf16x8 xr[MAXV], dr[MAXV], ar[MAXV];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vc = min(lane + 64 * k, nv - 1);
+    xr[k] = ld8(L.x3 + row * L.ldx3 + vc * 8);
+    dr[k] = ld8(L.dl + row * L.lddl + vc * 8);
+    ar[k] = ld8(L.add + row * L.ldadd + vc * 8);
+  }
   float xh[MAXV][8], gg[MAXV][8];
   float sa = 0.0f, sb = 0.0f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int vi = lane + 64 * k;
     if (vi < nv) {
-      float f[8], d[8];
-      load8(L.x3 + row * L.ldx3 + vi * 8, f);
-      load8(L.dl + row * L.lddl + vi * 8, d);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        xh[k][i] = (f[i] - mu) * rs;
-        gg[k][i] = d[i];
+        xh[k][i] = ((float)xr[k][i] - mu) * rs;
+        gg[k][i] = (float)dr[k][i];
         sa += gg[k][i];
         sb += gg[k][i] * xh[k][i];
       }
@@ -351,10 +378,9 @@ __device__ __forceinline__ void ln3_bwd_row(const Ln3Bwd& L, long row, int c, in
   for (int k = 0; k < MAXV; ++k) {
     const int vi = lane + 64 * k;
     if (vi < nv) {
-      float o[8], e[8];
-      load8(L.add + row * L.ldadd + vi * 8, e);
+      float o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)(rs * (gg[k][i] - ma - xh[k][i] * mb)) + e[i];
+      for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)(rs * (gg[k][i] - ma - xh[k][i] * mb)) + (float)ar[k][i];
       store8(out + vi * 8, o);
     }
   }
@@ -371,7 +397,11 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
   __shared__ float s_red[NW][kRows][2];
   __shared__ float s_tile[NW][kRows][17];
   __shared__ __attribute__((aligned(16))) bf16 s_dy[LN3 ? kRows : 1][LN3 ? kDyLd : 8];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
+  // gamma and the block's probabilities staged once (as in the forward: per-tile / post-barrier global reads were
+  // dependent round trips)
+  __shared__ float s_gam[Fit<NW>::MAXC];
+  __shared__ float s_prob[kRows][kHP];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, r = lane & 15, g = lane >> 4;
   const long row0 = (long)blockIdx.x * kRows;
   const long row = row0 + r;
   const bool ok = row < rows;
@@ -380,6 +410,20 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
   const int rr = lane >> 2, cc = (lane & 3) * 4;
   const long orow = row0 + rr;
   const Tabs T(tabs, c);
+  float gst[kStage<NW>];
+#pragma unroll
+  for (int k = 0; k < kStage<NW>; ++k) gst[k] = gamma[min((int)threadIdx.x + 64 * NW * k, c - 1)];
+  static_assert(64 * NW >= kRows * kHP, "one staged probability per thread");
+  const int pro = threadIdx.x / kHP, phh = threadIdx.x - pro * kHP;
+  const float pst = probs[min((row0 + min(pro, kRows - 1)) * heads + min(phh, heads - 1), rows * heads - 1)];
+  auto stage = [&]() {
+#pragma unroll
+    for (int k = 0; k < kStage<NW>; ++k) {
+      const int i = threadIdx.x + 64 * NW * k;
+      if (i < c) s_gam[i] = gst[k];
+    }
+    if (pro < kRows) s_prob[pro][phh] = pst;
+  };
   if constexpr (LN3) {
     // phase 0: dy of the block's rows (norm3 backward + residual) into the LDS tile
     for (int q = w; q < kRows; q += NW) {
@@ -388,6 +432,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
         else ln3_bwd_row<3>(ln3, row0 + q, c, lane, &s_dy[q][0]);
       }
     }
+    stage();
     __syncthreads();
   }
   // dy row r / rr of the block: the LDS tile (LN3) or global memory
@@ -396,16 +441,9 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
     else return dy + rg * lddy + col;
   };
   // phase 1: G = dy . D^T over the wave's channel chunks (dy is exactly bf16)
-  bf16x8 av[MK];
+  bf16x8 av[MK];   // unconditional loads, chunks past the wave's last skipped at their use (see the forward)
 #pragma unroll
-  for (int i = 0; i < MK; ++i) {
-    if (kb + i < ke && ok) {
-      av[i] = ld8(dy_at(r, row, (kb + i) * 32 + g * 8));
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) av[i][j] = (bf16)0.0f;
-    }
-  }
+  for (int i = 0; i < MK; ++i) av[i] = ld8(dy_at(r, ok ? row : rows - 1, min(kb + i, ke - 1) * 32 + g * 8));
   bf16x8 bk[MK][2][2];
   load_k<MK>(kb, ke, T.dh, T.dl, c, r, g, bk);
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -426,6 +464,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
   for (int ht = 0; ht < 2; ++ht)
 #pragma unroll
     for (int e = 0; e < 4; ++e) s_part[w][g * 4 + e][ht * 16 + r] = acc[ht][e];
+  if constexpr (!LN3) stage();
   __syncthreads();
   for (int i = threadIdx.x; i < kRows * kHP; i += 64 * NW) {
     const int ro = i / kHP, hh = i - ro * kHP;
@@ -434,7 +473,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
     for (int v = 0; v < NW; ++v) gs += s_part[v][ro][hh];
     float dsg = 0.0f;
     if (hh < heads && row0 + ro < rows) {
-      const float p = probs[(row0 + ro) * heads + hh];
+      const float p = s_prob[ro][hh];
       dsg = gs * p * (1.0f - p);
     }
     s_sig[ro][hh] = dsg;
@@ -466,7 +505,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
       for (int j = 0; j < 4; ++j) {
         const int col = ct * 16 + cc + j;
         const float xh = ((float)xw[t][j] - mu) * rs;
-        dn[t][j] = (float)(bf16)s_tile[w][rr][cc + j] * gamma[col];
+        dn[t][j] = (float)(bf16)s_tile[w][rr][cc + j] * s_gam[col];
         if (orow < rows) {
           sa += dn[t][j];
           sb += dn[t][j] * xh;

@@ -58,9 +58,29 @@ def main():
     torch.cuda.synchronize()
     t_eager = e0.elapsed_time(e1)
 
+    # one replay alone (best of 5) against a back-to-back chain of 50, both between HIP events
+    one = []
+    for _ in range(5):
+        pipe.ctx.step.zero_()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        one.append(e0.elapsed_time(e1))
+    pipe.ctx.step.zero_()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(50):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    chain = e0.elapsed_time(e1) / 50
+
     print(f"full call {t_call*1e3:.1f} ms | 50 graph replays {t_graph*1e3:.1f} ms (host enqueue {t_host*1e3:.1f} ms)"
           f" -> {t_graph / 50 * 1e3:.2f} ms/step | eager step {t_eager:.2f} ms | per-call overhead "
-          f"~{(t_call - t_graph) * 1e3:.1f} ms", flush=True)
+          f"~{(t_call - t_graph) * 1e3:.1f} ms | one replay {min(one):.3f} ms (events, best of 5), chained "
+          f"{chain:.3f} ms/replay", flush=True)
 
 
 if __name__ == "__main__":
