@@ -881,22 +881,40 @@ extern "C" int dc_groupnorm_bwd_acc(const void* x, int ldx, const void* x2, int 
 // ---------------------------------------------------------------- LayerNorm (one wave per row)
 namespace {
 
+// Every global load of a row is issued before the first use (clamped segment index: lanes past the row's end re-read
+// its last segment and skip it at every use; the per-channel vectors as 16-B loads).  Guarded by the lane condition,
+// the loads sat in divergent branches that the compiler closed with a wait each -- ~10-45 dependent round trips per
+// row (profiles/r06s).
 template <int MAXV>
-__global__ void ln_fwd_kernel(const bf16* x, int ldx, long rows, int c, float eps, const float* gamma,
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16* x, int ldx, long rows, int c, float eps, const float* gamma,
                               const float* beta, bf16* y, int ldy, float* stats) {
   const long row = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int nv = c >> 3;
+  bf16x8 xr[MAXV];
+  f32x4 ga[MAXV][2], be[MAXV][2];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vc = min(lane + 64 * k, nv - 1);
+    xr[k] = *reinterpret_cast<const bf16x8*>(x + row * ldx + vc * 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ga[k][h] = *reinterpret_cast<const f32x4*>(gamma + vc * 8 + 4 * h);
+      be[k][h] = *reinterpret_cast<const f32x4*>(beta + vc * 8 + 4 * h);
+    }
+  }
   float v[MAXV][8];
   float s = 0.0f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int vi = lane + 64 * k;
     if (vi < nv) {
-      load8(x + row * ldx + vi * 8, v[k]);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s += v[k][i];
+      for (int i = 0; i < 8; ++i) {
+        v[k][i] = (float)xr[k][i];
+        s += v[k][i];
+      }
     }
   }
   const float mu = wave_sum(s) / c;
@@ -916,7 +934,7 @@ __global__ void ln_fwd_kernel(const bf16* x, int ldx, long rows, int c, float ep
     if (vi < nv) {
       float o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * gamma[vi * 8 + i] + beta[vi * 8 + i];
+      for (int i = 0; i < 8; ++i) o[i] = (v[k][i] - mu) * rs * ga[k][i >> 2][i & 3] + be[k][i >> 2][i & 3];
       store8(y + row * ldy + vi * 8, o);
     }
   }
@@ -927,27 +945,36 @@ __global__ void ln_fwd_kernel(const bf16* x, int ldx, long rows, int c, float ep
 }
 
 template <int MAXV>
-__global__ void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const float* gamma, const float* stats,
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const float* gamma, const float* stats,
                               const bf16* dy, int lddy, bf16* dx, int lddx, const bf16* add, int ldadd) {
   const long row = (long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
   const int nv = c >> 3;
   const float mu = stats[row * 2], rs = stats[row * 2 + 1];
-  float xh[MAXV][8], g[MAXV][8], ad[MAXV][8];
+  bf16x8 xr[MAXV], dr[MAXV], ar[MAXV];
+  f32x4 ga[MAXV][2];
+#pragma unroll
+  for (int k = 0; k < MAXV; ++k) {
+    const int vc = min(lane + 64 * k, nv - 1);
+    xr[k] = *reinterpret_cast<const bf16x8*>(x + row * ldx + vc * 8);
+    dr[k] = *reinterpret_cast<const bf16x8*>(dy + row * lddy + vc * 8);
+    if (add) ar[k] = *reinterpret_cast<const bf16x8*>(add + row * ldadd + vc * 8);
+    if (gamma) {   // NULL: dy is gamma * dL/dy already
+#pragma unroll
+      for (int h = 0; h < 2; ++h) ga[k][h] = *reinterpret_cast<const f32x4*>(gamma + vc * 8 + 4 * h);
+    }
+  }
+  float xh[MAXV][8], g[MAXV][8];
   float sa = 0.0f, sb = 0.0f;
 #pragma unroll
   for (int k = 0; k < MAXV; ++k) {
     const int vi = lane + 64 * k;
     if (vi < nv) {
-      float f[8], d[8];
-      load8(x + row * ldx + vi * 8, f);
-      load8(dy + row * lddy + vi * 8, d);
-      if (add) load8(add + row * ldadd + vi * 8, ad[k]);   // with the other loads: one round trip
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        xh[k][i] = (f[i] - mu) * rs;
-        g[k][i] = gamma ? d[i] * gamma[vi * 8 + i] : d[i];   // gamma NULL: dy is gamma * dL/dy already
+        xh[k][i] = ((float)xr[k][i] - mu) * rs;
+        g[k][i] = gamma ? (float)dr[k][i] * ga[k][i >> 2][i & 3] : (float)dr[k][i];
         sa += g[k][i];
         sb += g[k][i] * xh[k][i];
       }
@@ -963,7 +990,7 @@ __global__ void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const fl
       for (int i = 0; i < 8; ++i) o[i] = rs * (g[k][i] - ma - xh[k][i] * mb);
       if (add) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)o[i] + ad[k][i];
+        for (int i = 0; i < 8; ++i) o[i] = (float)(bf16)o[i] + (float)ar[k][i];
       }
       store8(dx + row * lddx + vi * 8, o);
     }
@@ -975,7 +1002,7 @@ __global__ void ln_bwd_kernel(const bf16* x, int ldx, long rows, int c, const fl
 extern "C" int dc_layernorm_fwd(const void* x, int ldx, long long rows, int c, float eps, const float* gamma,
                                 const float* beta, void* y, int ldy, float* stats, void* stream) {
   if (!x || !y || !gamma || !beta || rows <= 0 || c <= 0 || c % 8 || c > 2048 * 8) return DC_ERR_ARG;
-  if (ldx % 8 || ldy % 8) return DC_ERR_ALIGN;
+  if (ldx % 8 || ldy % 8 || ((uintptr_t)gamma & 15) || ((uintptr_t)beta & 15)) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   const int wpb = 4;
   dim3 grid((unsigned)((rows + wpb - 1) / wpb));
@@ -999,7 +1026,7 @@ extern "C" int dc_layernorm_bwd(const void* x, int ldx, long long rows, int c, c
                                 const void* dy, int lddy, void* dx, int lddx, const void* add, int ldadd,
                                 void* stream) {
   if (!x || !dy || !dx || !stats || rows <= 0 || c <= 0 || c % 8) return DC_ERR_ARG;
-  if (ldx % 8 || lddy % 8 || lddx % 8 || (add && ldadd % 8)) return DC_ERR_ALIGN;
+  if (ldx % 8 || lddy % 8 || lddx % 8 || (add && ldadd % 8) || ((uintptr_t)gamma & 15)) return DC_ERR_ALIGN;
   hipStream_t st = (hipStream_t)stream;
   const int wpb = 4;
   dim3 grid((unsigned)((rows + wpb - 1) / wpb));
