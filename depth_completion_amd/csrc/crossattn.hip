@@ -164,10 +164,11 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_fwd_kernel(const bf16* x, 
   // every load unconditional (a row past the end reads the last row; nothing of it is stored): a load guarded by a
   // lane condition sits in a divergent branch, and the compiler waits for it before leaving the branch
   const long rowc = ok ? row : rows - 1;
-  // (chunks past the wave's last re-read it and are skipped at every use)
+  // (chunks past the wave's last -- all of them for a wave without chunks, C < 32 NW -- re-read the row's last chunk and
+  // are skipped at every use)
   bf16x8 xv[MK];
 #pragma unroll
-  for (int i = 0; i < MK; ++i) xv[i] = ld8(x + rowc * ldx + min(kb + i, ke - 1) * 32 + g * 8);
+  for (int i = 0; i < MK; ++i) xv[i] = ld8(x + rowc * ldx + min(kb + i, nk - 1) * 32 + g * 8);
   bf16x8 bk[MK][2][2];
   load_k<MK>(kb, ke, T.uh, T.ul, c, r, g, bk);
   float aff[3][kStage<NW>];
@@ -443,7 +444,7 @@ __global__ __launch_bounds__(64 * NW) void cross_mfma_bwd_kernel(const bf16* x, 
   // phase 1: G = dy . D^T over the wave's channel chunks (dy is exactly bf16)
   bf16x8 av[MK];   // unconditional loads, chunks past the wave's last skipped at their use (see the forward)
 #pragma unroll
-  for (int i = 0; i < MK; ++i) av[i] = ld8(dy_at(r, ok ? row : rows - 1, min(kb + i, ke - 1) * 32 + g * 8));
+  for (int i = 0; i < MK; ++i) av[i] = ld8(dy_at(r, ok ? row : rows - 1, min(kb + i, nk - 1) * 32 + g * 8));
   bf16x8 bk[MK][2][2];
   load_k<MK>(kb, ke, T.dh, T.dl, c, r, g, bk);
   f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};

@@ -369,7 +369,8 @@ def test_linear_ln_fused(ctx, c, n, geglu, algo, nsplit):
         assert rel(dx, xr.grad) < 2e-2
 
 
-@pytest.mark.parametrize("C,heads", [(320, 5), (640, 10), (1280, 20)])
+# (64, 1) / (128, 2): the tiny UNet widths, where most waves of the block own no channel chunk
+@pytest.mark.parametrize("C,heads", [(64, 1), (128, 2), (320, 5), (640, 10), (1280, 20)])
 def test_cross_bwd_ln3_fused(ctx, C, heads):
     """dc_crossattn_bwd_ln (norm3 backward computed in the cross-attention backward's launch) equals
     dc_layernorm_bwd (gamma folded) followed by dc_crossattn_bwd bit for bit, ragged row count included."""
@@ -499,7 +500,7 @@ def test_attention_bwd_stream_k(ctx, n, t, heads, monkeypatch):
     assert rel(outs["2"].view(n, t, 3 * C), qkv.grad) < 2e-2
 
 
-@pytest.mark.parametrize("C,heads", [(320, 5), (640, 10), (1280, 20)])
+@pytest.mark.parametrize("C,heads", [(64, 1), (128, 2), (320, 5), (640, 10), (1280, 20)])
 def test_cross_attention_fold(ctx, C, heads):
     """Folded 2-key cross-attention == LN2 + attn2 (2-token context) + residual; the three UNet widths
     (U and D staged together in LDS at 320 / 640, one after the other at 1280 x 20 heads)."""
