@@ -60,6 +60,26 @@ __global__ void upsample_adjoint_kernel(const bf16* dhi, int ldhi, int nb, int h
     const int y0 = (int)(((long)Y * hhi + hlo - 1) / hlo), y1 = (int)(((long)(Y + 1) * hhi + hlo - 1) / hlo);
     const int x0 = (int)(((long)X * whi + wlo - 1) / wlo), x1 = (int)(((long)(X + 1) * whi + wlo - 1) / wlo);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (y1 - y0 == 2 && x1 - x0 == 2) {
+      // the UNet's exact 2x: the four loads (and the mask's) in flight together, summed in the loop's order
+      bf16x8 q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        q[j] = *reinterpret_cast<const bf16x8*>(dhi + (((long)n * hhi + y0 + (j >> 1)) * whi + x0 + (j & 1)) * ldhi +
+                                                g * 8);
+      bf16x8 mq;
+      if (mask) mq = *reinterpret_cast<const bf16x8*>(mask + pix * ldmask + g * 8);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += (float)q[j][k];
+      if (mask) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = (float)mq[k] > 0.0f ? acc[k] : 0.0f;
+      }
+      store8(dlo + pix * ldlo + g * 8, acc);
+      continue;
+    }
     for (int y = y0; y < y1; ++y)
       for (int x = x0; x < x1; ++x) {
         float v[8];
@@ -96,14 +116,23 @@ __global__ void taesd_clamp_fwd_kernel(const bf16* x, int ldx, long P, bf16* y) 
 //   gx0 -> gx_direct = gx0*sqrt(a) (bf16), dv = -gx0*sqrt(b) (bf16, into dv[P][8], 4..7 zero)
 __global__ void taesd_clamp_bwd_kernel(const bf16* x0, int ldx0, const bf16* dy, int lddy, long P, const float* coef,
                                        const int* step, bf16* gx_direct, bf16* dv) {
+  // the first pixel's rows go out before the step's dependent coefficient reads (8-B vectors; clamped, skipped)
+  long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  bf16x4 xr = *reinterpret_cast<const bf16x4*>(x0 + min(p, P - 1) * ldx0);
+  bf16x4 dr = *reinterpret_cast<const bf16x4*>(dy + min(p, P - 1) * lddy);
+  asm volatile("" ::: "memory");
   const float sa = coef[*step * 4 + 0], sb = coef[*step * 4 + 1];
-  for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (long)gridDim.x * blockDim.x) {
+  for (bool first = true; p < P; p += (long)gridDim.x * blockDim.x, first = false) {
+    if (!first) {
+      xr = *reinterpret_cast<const bf16x4*>(x0 + p * ldx0);
+      dr = *reinterpret_cast<const bf16x4*>(dy + p * lddy);
+    }
     float gd[8], vv[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float a = (float)(bf16)((float)x0[p * ldx0 + k] / 3.0f);
+      const float a = (float)(bf16)((float)xr[k] / 3.0f);
       const float t = (float)(bf16)tanhf(a);
-      float g = (float)(bf16)((float)dy[p * lddy + k] * 3.0f);
+      float g = (float)(bf16)((float)dr[k] * 3.0f);
       g = (float)(bf16)(g * (1.0f - t * t));
       g = (float)(bf16)(g / 3.0f);
       gd[k] = g * sa;
@@ -247,6 +276,7 @@ extern "C" int dc_taesd_clamp_fwd(const void* x, int ldx, long long pixels, void
 extern "C" int dc_taesd_clamp_bwd(const void* x0, int ldx0, const void* dy, int lddy, long long pixels,
                                   const float* coef, const int* step, void* gx_direct, void* dv, void* stream) {
   if (!x0 || !dy || !coef || !step || !gx_direct || !dv || pixels <= 0) return DC_ERR_ARG;
+  if (ldx0 % 4 || lddy % 4 || ((uintptr_t)x0 & 7) || ((uintptr_t)dy & 7)) return DC_ERR_ALIGN;
   hipLaunchKernelGGL(taesd_clamp_bwd_kernel, grid_for(pixels), dim3(256), 0, (hipStream_t)stream, (const bf16*)x0,
                      ldx0, (const bf16*)dy, lddy, (long)pixels, coef, step, (bf16*)gx_direct, (bf16*)dv);
   DC_CHECK_LAUNCH();

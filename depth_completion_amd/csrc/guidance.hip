@@ -165,27 +165,46 @@ __global__ void preview_kernel(const bf16* x8, const bf16* v, int hw, const floa
                                bf16* tin, float* eps_norm) {
   __shared__ float scratch[16];
   const int n = blockIdx.x;
-  const float sa = coef[*step * 4 + 0], sb = coef[*step * 4 + 1];
+  // one block per frame (the norm below is a block sum): each thread's pixels are loaded kPf at a time, all of them
+  // before the coefficients' dependent reads -- one pixel per round trip made this launch ~20 us at C2
+  constexpr int kPf = 8;
   float ss = 0.0f;
-  for (int p = threadIdx.x; p < hw; p += blockDim.x) {
-    const long pix = (long)n * hw + p;
-    float xo[8], to[8];
+  float sa = 0.0f, sb = 0.0f;
+  for (int p0 = threadIdx.x; p0 < hw; p0 += kPf * blockDim.x) {
+    bf16x8 xr[kPf], vr[kPf];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float x = (float)x8[pix * 8 + 4 + k];
-      const float vv = (float)v[pix * 8 + k];
-      const float t1 = (float)(bf16)(sa * x), t2 = (float)(bf16)(sb * vv);
-      const float xz = (float)(bf16)(t1 - t2);
-      const float e = (float)(bf16)((float)(bf16)(sa * vv) + (float)(bf16)(sb * x));
-      ss += e * e;
-      xo[k] = xz;
-      xo[k + 4] = 0.0f;
-      const float a = (float)(bf16)(xz / 3.0f);
-      to[k] = (float)(bf16)((float)(bf16)tanhf(a) * 3.0f);
-      to[k + 4] = 0.0f;
+    for (int u = 0; u < kPf; ++u) {
+      const long pix = (long)n * hw + min(p0 + u * (int)blockDim.x, hw - 1);
+      xr[u] = *reinterpret_cast<const bf16x8*>(x8 + pix * 8);
+      vr[u] = *reinterpret_cast<const bf16x8*>(v + pix * 8);
     }
-    store8(x0 + pix * 8, xo);
-    store8(tin + pix * 8, to);
+    if (p0 == (int)threadIdx.x) {
+      sa = coef[*step * 4 + 0];
+      sb = coef[*step * 4 + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kPf; ++u) {
+      const int p = p0 + u * blockDim.x;
+      if (p >= hw) continue;
+      const long pix = (long)n * hw + p;
+      float xo[8], to[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x = (float)xr[u][4 + k];
+        const float vv = (float)vr[u][k];
+        const float t1 = (float)(bf16)(sa * x), t2 = (float)(bf16)(sb * vv);
+        const float xz = (float)(bf16)(t1 - t2);
+        const float e = (float)(bf16)((float)(bf16)(sa * vv) + (float)(bf16)(sb * x));
+        ss += e * e;
+        xo[k] = xz;
+        xo[k + 4] = 0.0f;
+        const float a = (float)(bf16)(xz / 3.0f);
+        to[k] = (float)(bf16)((float)(bf16)tanhf(a) * 3.0f);
+        to[k + 4] = 0.0f;
+      }
+      store8(x0 + pix * 8, xo);
+      store8(tin + pix * 8, to);
+    }
   }
   const float tot = block_sum(ss, scratch);
   if (threadIdx.x == 0) eps_norm[n] = (float)(bf16)sqrtf(tot);
@@ -300,6 +319,11 @@ __global__ void sparse_loss_kernel(const bf16* out, int ldo, int PH, int PW, int
   __shared__ float scratch[16];
   const int n = blockIdx.x;
   const long HW = (long)H * W;
+  // the thread's first point index and guide go out with the count and the parameters (a clamped slot, used only
+  // when it is a point): not after the count, one round trip less
+  const long k0 = min((long)threadIdx.x, HW - 1);
+  const int p0 = idx[n * HW + k0];
+  const float g0 = gval[n * HW + k0];
   const int count = cnt[n];
   const float* pr = params + n * 8;
   const float gmin = pr[4], gmax = pr[5];
@@ -312,14 +336,15 @@ __global__ void sparse_loss_kernel(const bf16* out, int ldo, int PH, int PW, int
   float* dAn = dA + (long)n * PH * PW;
   const DSpace ds(pr);
   for (int k = threadIdx.x; k < count; k += blockDim.x) {
-    const int p = idx[n * HW + k];
+    const bool first = k == (int)threadIdx.x;
+    const int p = first ? p0 : idx[n * HW + k];
     const int y = p / W, x = p - (p / W) * W;
     Taps t;
     const float aff = sample_affine(out, ldo, n, PH, PW, RH, RW, H, W, y, x, t, interp_nearest(pr));
     const float F = B * aff + E;
     float dNdG;
     const float Nv = ds(fminf(fmaxf(F, 0.0f), 1.0f), dNdG);
-    const float r = Nv - gval[n * HW + k];
+    const float r = Nv - (first ? g0 : gval[n * HW + k]);
     lsum += fabsf(r) * inv_cnt + (r * r) * inv_cnt;
     const float sg = (r > 0.0f) ? 1.0f : ((r < 0.0f) ? -1.0f : 0.0f);
     const float dG = (sg * inv_cnt + 2.0f * r * inv_cnt) * dNdG;
@@ -396,21 +421,17 @@ struct UpdCtx {
   float sa, sb, sap, sbp, step_size, bc2s, step_aff;
   int opt;
 };
-__device__ __forceinline__ void latent_elem_update(const UpdCtx& u, bf16* x8, const bf16* v, bf16* m_lat, bf16* v_lat,
-                                                   long pix, int k, float g) {
+// the arithmetic on values (x: the latent, vm: v, g: the rescaled gradient; m / vv: the optimiser state, updated in
+// place as the rule writes it): returns the new latent
+__device__ __forceinline__ float latent_elem_core(const UpdCtx& u, float x, float vm, float g, float& m, float& vv) {
   const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
   const float sa = u.sa, sb = u.sb, sap = u.sap, sbp = u.sbp, step_size = u.step_size, bc2s = u.bc2s;
   const int opt = u.opt;
-  const long e = pix * 4 + k;
-  const float x = (float)x8[pix * 8 + 4 + k];
   float xp;
   if (opt == 0) {
-    float m = (float)m_lat[e], vv = (float)v_lat[e];
     m = (float)(bf16)(m + beta1w * (g - m));
     vv = (float)(bf16)(vv * beta2);
     vv = (float)(bf16)(vv + one_m_b2 * g * g);
-    m_lat[e] = (bf16)m;
-    v_lat[e] = (bf16)vv;
     float den = (float)(bf16)sqrtf(vv);
     den = (float)(bf16)(den / bc2s);
     den = (float)(bf16)(den + eps);
@@ -418,16 +439,24 @@ __device__ __forceinline__ void latent_elem_update(const UpdCtx& u, bf16* x8, co
   } else if (opt == 1) {
     xp = (float)(bf16)(x + (-step_size) * g);
   } else {
-    float sum = (float)(bf16)((float)m_lat[e] + g * g);
-    m_lat[e] = (bf16)sum;
+    const float sum = (float)(bf16)(m + g * g);
+    m = sum;
     const float sd = (float)(bf16)((float)(bf16)sqrtf(sum) + 1e-10f);
     xp = (float)(bf16)(x + (-step_size) * (g / sd));
   }
-  const float vm = (float)v[pix * 8 + k];
   const float x0 = (float)(bf16)((float)(bf16)(sa * xp) - (float)(bf16)(sb * vm));
   const float ep = (float)(bf16)((float)(bf16)(sa * vm) + (float)(bf16)(sb * xp));
   const float dir = (float)(bf16)(sbp * ep);
-  const float prev = (float)(bf16)((float)(bf16)(sap * x0) + dir);
+  return (float)(bf16)((float)(bf16)(sap * x0) + dir);
+}
+__device__ __forceinline__ void latent_elem_update(const UpdCtx& u, bf16* x8, const bf16* v, bf16* m_lat, bf16* v_lat,
+                                                   long pix, int k, float g) {
+  const long e = pix * 4 + k;
+  float m = u.opt == 1 ? 0.0f : (float)m_lat[e];
+  float vv = u.opt == 0 ? (float)v_lat[e] : 0.0f;
+  const float prev = latent_elem_core(u, (float)x8[pix * 8 + 4 + k], (float)v[pix * 8 + k], g, m, vv);
+  if (u.opt != 1) m_lat[e] = (bf16)m;
+  if (u.opt == 0) v_lat[e] = (bf16)vv;
   x8[pix * 8 + 4 + k] = (bf16)prev;
 }
 
@@ -437,9 +466,13 @@ __device__ __forceinline__ void affine_update(const UpdCtx& u, int n, int j, con
   const float beta1w = 0.1f, beta2 = 0.999f, one_m_b2 = 0.001f, eps = 1e-8f;
   const int opt = u.opt;
   const float step_aff = u.step_aff, bc2s = u.bc2s;
+  // all four reads before the first store (a read after a store to a possibly aliasing pointer is one more round
+  // trip)
   const float g = daff_grad[n * 2 + j];
+  const float a = affine[n * 2 + j];
+  float m = opt != 1 ? m_aff[n * 2 + j] : 0.0f;
+  float vv = opt == 0 ? v_aff[n * 2 + j] : 0.0f;
   if (opt == 0) {
-    float m = m_aff[n * 2 + j], vv = v_aff[n * 2 + j];
     m = m + beta1w * (g - m);
     vv = vv * beta2;
     vv = vv + one_m_b2 * g * g;
@@ -448,13 +481,13 @@ __device__ __forceinline__ void affine_update(const UpdCtx& u, int n, int j, con
     float den = sqrtf(vv);
     den = den / bc2s;
     den = den + eps;
-    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (m / den);
+    affine[n * 2 + j] = a + (-step_aff) * (m / den);
   } else if (opt == 1) {
-    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * g;
+    affine[n * 2 + j] = a + (-step_aff) * g;
   } else {
-    const float sum = m_aff[n * 2 + j] + g * g;
+    const float sum = m + g * g;
     m_aff[n * 2 + j] = sum;
-    affine[n * 2 + j] = affine[n * 2 + j] + (-step_aff) * (g / (sqrtf(sum) + 1e-10f));
+    affine[n * 2 + j] = a + (-step_aff) * (g / (sqrtf(sum) + 1e-10f));
   }
 }
 
@@ -529,12 +562,17 @@ __global__ void latent_norm_kernel(const bf16* x8, const bf16* gdir, const bf16*
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const Kld kl{kld_mode, kld_weight, 0.0f, 1.0f, 1.0f / (4.0f * hw)};
   float ss = 0.0f;
+  // the pixel's rows as 16-B loads, unconditional (clamped pixel; skipped below): lane-guarded 2-B loads were one
+  // wait each
+  const long pix = (long)n * hw + min(p, hw - 1);
+  const bf16x8 gd = *reinterpret_cast<const bf16x8*>(gdir + pix * 8);
+  const bf16x8 gu = *reinterpret_cast<const bf16x8*>(gunet + pix * 8);
+  const bf16x8 xr = *reinterpret_cast<const bf16x8*>(x8 + pix * 8);
   if (p < hw) {
-    const long pix = (long)n * hw + p;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float g = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
-      if (kld_mode) g = (float)(bf16)(g + kl.grad((float)x8[pix * 8 + 4 + k]));
+      float g = (float)(bf16)((float)gd[k] + (float)gu[k]);
+      if (kld_mode) g = (float)(bf16)(g + kl.grad((float)xr[4 + k]));
       ss += g * g;
     }
   }
@@ -549,6 +587,17 @@ __global__ void latent_apply_kernel(bf16* x8, const bf16* v, const bf16* gdir, c
                                     const float* part) {
   __shared__ float s_ss;
   const int n = blockIdx.y, nblk = gridDim.x;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  // every read of the pixel first (16-B rows, 8-B optimiser state; clamped pixel, skipped below), ahead of the
+  // partials' fold and the step's coefficient reads: read per element between the element stores they were ~8
+  // dependent round trips
+  const long pix = (long)n * hw + min(p, hw - 1);
+  const bf16x8 gd = *reinterpret_cast<const bf16x8*>(gdir + pix * 8);
+  const bf16x8 gu = *reinterpret_cast<const bf16x8*>(gunet + pix * 8);
+  const bf16x8 xr = *reinterpret_cast<const bf16x8*>(x8 + pix * 8);
+  const bf16x8 vr = *reinterpret_cast<const bf16x8*>(v + pix * 8);
+  const bf16x4 mr = *reinterpret_cast<const bf16x4*>(m_lat + pix * 4);
+  const bf16x4 wr = *reinterpret_cast<const bf16x4*>(v_lat + pix * 4);
   if (threadIdx.x < 64) {
     float t = 0.0f;
     for (int b = threadIdx.x; b < nblk; b += 64) t += part[(long)n * nblk + b];
@@ -564,17 +613,20 @@ __global__ void latent_apply_kernel(bf16* x8, const bf16* v, const bf16* gdir, c
   const float gnc = gn < 1e-7f ? (float)(bf16)1e-7f : gn;
   const float factor = (float)(bf16)(en / gnc);
   const Kld kl{kld_mode, kld_weight, 0.0f, 1.0f, 1.0f / (4.0f * hw)};
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < hw) {
-    const long pix = (long)n * hw + p;
-    float g[4];
+    bf16x4 xo, mo, wo;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {   // all reads of x before the in-place update of this pixel
-      g[k] = (float)(bf16)((float)gdir[pix * 8 + k] + (float)gunet[pix * 8 + k]);
-      if (kld_mode) g[k] = (float)(bf16)(g[k] + kl.grad((float)x8[pix * 8 + 4 + k]));
+    for (int k = 0; k < 4; ++k) {
+      float g = (float)(bf16)((float)gd[k] + (float)gu[k]);
+      if (kld_mode) g = (float)(bf16)(g + kl.grad((float)xr[4 + k]));
+      float m = (float)mr[k], vv = (float)wr[k];
+      xo[k] = (bf16)latent_elem_core(u, (float)xr[4 + k], (float)vr[k], (float)(bf16)(g * factor), m, vv);
+      mo[k] = (bf16)m;
+      wo[k] = (bf16)vv;
     }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) latent_elem_update(u, x8, v, m_lat, v_lat, pix, k, (float)(bf16)(g[k] * factor));
+    *reinterpret_cast<bf16x4*>(x8 + pix * 8 + 4) = xo;
+    if (opt != 1) *reinterpret_cast<bf16x4*>(m_lat + pix * 4) = mo;
+    if (opt == 0) *reinterpret_cast<bf16x4*>(v_lat + pix * 4) = wo;
   }
   if (blockIdx.x == 0 && threadIdx.x < 2) affine_update(u, n, threadIdx.x, daff_grad, affine, m_aff, v_aff);
   if (dbg && blockIdx.x == 0 && threadIdx.x == 0) {

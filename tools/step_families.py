@@ -19,3 +19,14 @@ for s,e,n in win:
 tot=sum(v[1] for v in agg.values())
 print(f"window {len(win)} kernels, busy {tot/1e3:.3f} ms, wall {(win[-1][1]-win[0][0])/1e6:.3f} ms")
 for k,(c,t) in sorted(agg.items(), key=lambda kv:-kv[1][1]): print(f"{k:30s} x{c:4d} {t:9.1f} us {100*t/tot:5.1f}%")
+# optional third argument "names": the same window per kernel name (template arguments kept)
+if len(sys.argv) > 3 and sys.argv[3] == "names":
+    byname = defaultdict(lambda: [0, 0.0])
+    for s, e, n in win:
+        k = n.replace("(anonymous namespace)::", "").replace("void ", "")
+        k = re.sub(r"\(.*", "", k)[:70]
+        byname[k][0] += 1
+        byname[k][1] += (e - s) / 1e3
+    print("-- per kernel name")
+    for k, (c, t) in sorted(byname.items(), key=lambda kv: -kv[1][1]):
+        print(f"{k:70s} x{c:4d} {t:9.1f} us")
