@@ -505,3 +505,26 @@ def test_graph_replay_new_frames_same_bucket():
     df, lf = fresh(ib.to(dev), sb.to(dev), 120.0, **kw)
     torch.cuda.synchronize()
     assert torch.equal(db, df) and torch.equal(lb, lf)
+
+
+def test_side_stream_shortcuts_bitwise(monkeypatch):
+    """DC_SIDE_STREAM=1 (the resnet shortcut convs as a concurrent branch of the captured step graph, their own stream
+    and workspace; off by default, measured slower, profiles/r06p) gives the single-stream results bit for bit: the
+    same kernels on the same operands, only the launch order differs."""
+    from depth_completion_amd.config import TINY
+    from depth_completion_amd.pipeline import MarigoldDepthCompletionPipeline
+    n, h, w = 1, 192, 256
+    cfg_o = tiny_unet_config()
+    imgs, sparses = synth_inputs(n, h, w, 40, seed=35)
+    _, usd, vsd, emb = build(cfg_o, TINY, torch.float32, ORACLE)
+    args = dict(norm="const", steps=4, resolution=256)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DC_SIDE_STREAM", mode)
+        pipe = MarigoldDepthCompletionPipeline(usd, vsd, emb, unet_config=TINY, device=dev)
+        d, lat = pipe(imgs.to(dev), sparses.to(dev), 120.0, **args)
+        torch.cuda.synchronize()
+        out[mode] = (d.cpu(), lat.cpu())
+        assert all((st["unet"].side is not None) == (mode == "1") for st in pipe._plans.values())
+    assert torch.equal(out["0"][0], out["1"][0])
+    assert torch.equal(out["0"][1].view(torch.int16), out["1"][1].view(torch.int16))
